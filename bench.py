@@ -1,0 +1,148 @@
+#!/usr/bin/env python
+"""Headline benchmark: BERT-base masked-LM DDP training throughput (tokens/s, whole job).
+
+BASELINE.json metric: "tokens/sec (whole node) BERT-base DDP at 1/2/4/8 MI355X".  The step
+timed here is the full training step of the reference's ``data_parallel_training.py``
+(forward with MLM labels -> backward with bucketed gradient all-reduce -> Adam step), on
+bert-base-cased geometry (108.3 M parameters, random init), seq 512, synthetic MLM batches
+with the reference masking law, bf16 compute with fp32 master weights.  Per-GPU batch is
+fixed as N grows (weak scaling).
+
+  python bench.py --gpus N --steps K --warmup W
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line; ``value`` = total tokens/s over all ranks, computed from the
+MAX step time over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="base")
+    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("DTD_BENCH_BATCH", "32")),
+                    help="per-GPU micro-batch (sequences)")
+    ap.add_argument("--seq-len", type=int, default=512)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--grad-dtype", default=None, choices=[None, "bf16", "fp32"])
+    ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("DTD_BUCKET_MB", "64")))
+    ap.add_argument("--impl", default="fused", choices=["fused", "reference"])
+    ap.add_argument("--dense-mlm-head", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from distributed_training_and_deepspeed_amd import comm
+    from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
+    from distributed_training_and_deepspeed_amd.models import build_model, get_config
+    from distributed_training_and_deepspeed_amd.optim import hf_adamw
+    from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
+
+    cuda = torch.cuda.is_available()
+    if cuda:
+        torch.cuda.set_device(local)
+    device = torch.device("cuda", local) if cuda else torch.device("cpu")
+    if world > 1:
+        comm.init(rank=rank, world_size=world, local_rank=local)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    cfg = get_config(args.model)
+    model = build_model(args.model, impl=args.impl, dtype=dtype, device=device, seed=1234,
+                        sparse_mlm_head=not args.dense_mlm_head)
+    model.train()
+    gdt = {"bf16": torch.bfloat16, "fp32": torch.float32}.get(args.grad_dtype, dtype)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt)
+    opt = hf_adamw(ddp.parameters(), lr=5e-5)
+
+    B, S = args.batch_size, args.seq_len
+    nb = args.warmup + args.steps
+    ds = SyntheticLMDataset(cfg, num_samples=B * min(nb, 8), seq_len=S, seed=100 + rank)
+    ids = ds.input_ids.view(-1, B, S).to(device)
+    labels = ds.labels.view(-1, B, S).to(device)
+    nbuf = ids.shape[0]
+
+    def step(i):
+        out = ddp(ids[i % nbuf], labels=labels[i % nbuf])
+        out.loss.backward()
+        opt.step()
+        model.rt.rng.advance()
+        return out.loss
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for i in range(args.warmup):
+        loss = step(i)
+    sync()
+    first_loss = float(loss) if args.warmup else float("nan")
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    sync()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    tokens = world * B * S * args.steps
+    value = tokens / dt
+    if rank == 0:
+        res = {
+            "metric": "tokens/sec (whole node) BERT-base DDP",
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (random token ids, HF MLM 15%/80/10/10 masking; random-init weights)",
+            "config": {
+                "model": cfg.name,
+                "params": sum(p.numel() for p in model.parameters()),
+                "global_batch": B * world,
+                "per_gpu_batch": B,
+                "seq_len": S,
+                "parallelism": f"dp{world}",
+                "bucket_mb": args.bucket_mb,
+                "grad_dtype": str(gdt).replace("torch.", ""),
+                "impl": args.impl,
+                "mlm_head": "dense" if args.dense_mlm_head else "sparse (labelled rows only; identical loss/grads)",
+                "optimizer": "fused AdamW (transformers.AdamW hyper-params, lr 5e-5)",
+            },
+            "loss_first": round(first_loss, 4),
+            "loss_last": round(float(loss), 4),
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        comm.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+"""Process-group bootstrap and communication helpers.
+
+Replaces the reference's ``create_process_group`` (data_parallel_training.py:15-23,
+pytorch_allreduce.py:7-15: env MASTER_ADDR=localhost / MASTER_PORT=12355 +
+init_process_group('nccl')) and DeepSpeed's ``init_distributed``.
+
+On MI355X the torch backend name ``"nccl"`` is RCCL: collectives run over the xGMI full mesh
+(7 point-to-point links per GPU inside a node).  ``init`` pins the HIP device of the local
+rank *before* creating the group and passes ``device_id`` so the RCCL communicator is created
+eagerly (no lazy first-collective stall inside the timed loop).  gloo is used for CPU runs
+and the multi-process CPU tests.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+from . import logger  # noqa: F401
+from .logger import (all_gather_into_tensor, all_reduce, all_to_all_single, barrier, broadcast,  # noqa: F401
+                     comms_logger, log_summary, reduce, reduce_scatter_tensor)
+
+
+def env_rank() -> int:
+    return int(os.environ.get("RANK", os.environ.get("LOCAL_RANK", "0")))
+
+
+def env_local_rank() -> int:
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def env_world_size() -> int:
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def default_backend() -> str:
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+def init(rank: int | None = None, world_size: int | None = None, backend: str | None = None,
+         master_addr: str | None = None, master_port: int | str | None = None, local_rank: int | None = None,
+         timeout_s: float = 1800.0) -> tuple[int, int]:
+    """Initialise the default process group (idempotent).  Returns (rank, world_size)."""
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    rank = env_rank() if rank is None else rank
+    world_size = env_world_size() if world_size is None else world_size
+    local_rank = env_local_rank() if local_rank is None else local_rank
+    if master_addr is not None or "MASTER_ADDR" not in os.environ:
+        os.environ["MASTER_ADDR"] = master_addr or "127.0.0.1"
+    if master_port is not None or "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(master_port or 12355)
+    backend = backend or default_backend()
+    if backend in ("rccl", "nccl"):
+        backend = "nccl"
+    kw = {}
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+        kw["device_id"] = torch.device("cuda", local_rank)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world_size,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return rank, world_size
+
+
+def destroy() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def rank() -> int:
+    return dist.get_rank() if dist.is_initialized() else 0
+
+
+def world_size() -> int:
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def is_initialized() -> bool:
+    return dist.is_initialized()

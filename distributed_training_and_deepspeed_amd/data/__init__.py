@@ -1,0 +1,2 @@
+from .sampler import DeviceBatchLoader, DistributedSampler  # noqa: F401
+from .synthetic import IGNORE_INDEX, SyntheticLMDataset, load_synthetic, mlm_mask_tokens  # noqa: F401

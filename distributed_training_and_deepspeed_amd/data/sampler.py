@@ -1,0 +1,110 @@
+"""Distributed sampling and batch loading.
+
+``DistributedSampler`` reproduces torch's semantics used by the reference
+(data_parallel_training.py:41, zero_dp_training.py:66): a permutation seeded
+with ``seed + epoch`` (shuffle=True default), padded by repetition to a multiple of the world
+size (drop_last=False), then ``indices[rank::world]``.
+
+``DeviceBatchLoader`` replaces the DataLoader hot path: it gathers a whole batch with one
+index_select on pinned host memory and issues a single non-blocking H2D copy per tensor on a
+side stream (double-buffered), so the input copy overlaps the previous step's compute.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+class DistributedSampler(torch.utils.data.Sampler):
+    def __init__(self, dataset, num_replicas: int | None = None, rank: int | None = None, shuffle: bool = True,
+                 seed: int = 0, drop_last: bool = False):
+        if num_replicas is None or rank is None:
+            import torch.distributed as dist
+            ws = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+            rk = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+            num_replicas = ws if num_replicas is None else num_replicas
+            rank = rk if rank is None else rank
+        self.dataset, self.num_replicas, self.rank = dataset, num_replicas, rank
+        self.shuffle, self.seed, self.drop_last, self.epoch = shuffle, seed, drop_last, 0
+        n = len(dataset)
+        if drop_last and n % num_replicas:
+            self.num_samples = math.ceil((n - num_replicas) / num_replicas)
+        else:
+            self.num_samples = math.ceil(n / num_replicas)
+        self.total_size = self.num_samples * num_replicas
+
+    def __iter__(self):
+        n = len(self.dataset)
+        if self.shuffle:
+            g = torch.Generator()
+            g.manual_seed(self.seed + self.epoch)
+            indices = torch.randperm(n, generator=g).tolist()
+        else:
+            indices = list(range(n))
+        if not self.drop_last:
+            pad = self.total_size - len(indices)
+            if pad <= len(indices):
+                indices += indices[:pad]
+            else:
+                indices += (indices * math.ceil(pad / len(indices)))[:pad]
+        else:
+            indices = indices[: self.total_size]
+        return iter(indices[self.rank:self.total_size:self.num_replicas])
+
+    def __len__(self):
+        return self.num_samples
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = epoch
+
+
+class DeviceBatchLoader:
+    """Iterate fixed-size batches of a tensor dataset directly onto a device."""
+
+    def __init__(self, dataset, batch_size: int, sampler=None, device="cpu", drop_last: bool = False,
+                 keys=("input_ids", "labels")):
+        self.dataset, self.batch_size, self.device = dataset, batch_size, torch.device(device)
+        self.sampler = sampler if sampler is not None else range(len(dataset))
+        self.drop_last, self.keys = drop_last, keys
+        pin = self.device.type == "cuda"
+        self._host = {k: getattr(dataset, k) for k in keys}
+        if pin:
+            self._host = {k: v.pin_memory() for k, v in self._host.items()}
+        self._stream = torch.cuda.Stream(self.device) if pin else None
+
+    def __len__(self):
+        n = len(self.sampler)
+        return n // self.batch_size if self.drop_last else math.ceil(n / self.batch_size)
+
+    def _batches(self):
+        idx = list(iter(self.sampler))
+        for i in range(0, len(idx), self.batch_size):
+            chunk = idx[i:i + self.batch_size]
+            if self.drop_last and len(chunk) < self.batch_size:
+                return
+            yield torch.as_tensor(chunk, dtype=torch.int64)
+
+    def _load(self, ix):
+        out = {}
+        for k, v in self._host.items():
+            b = v.index_select(0, ix)
+            if self._stream is not None:
+                b = b.pin_memory()
+                with torch.cuda.stream(self._stream):
+                    out[k] = b.to(self.device, non_blocking=True)
+            else:
+                out[k] = b.to(self.device)
+        return out
+
+    def __iter__(self):
+        nxt = None
+        for ix in self._batches():
+            cur = self._load(ix) if nxt is None else nxt
+            if self._stream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self._stream)
+                for t in cur.values():
+                    t.record_stream(torch.cuda.current_stream(self.device))
+            nxt = None
+            yield cur
+        return

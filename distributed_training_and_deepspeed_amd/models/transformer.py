@@ -1,0 +1,260 @@
+"""Transformer layer with two interchangeable implementations.
+
+* ``fused`` (GPU, bf16/fp32): one autograd node per layer with a hand-written backward that
+  calls the gfx950 HIP kernels (flash attention, residual+dropout+LayerNorm, activation with
+  fused bias-gradient partials) and hipBLASLt GEMMs, writing weight gradients straight into
+  the flat gradient buckets (``ops/grad.py``).  Activations saved per layer: the layer input,
+  qkv, attention context + LSE, the two LayerNorm pre-normalisation sums with their row
+  statistics, and the FFN pre-activation -- dropout masks are regenerated, attention scores
+  are never materialised.
+* ``reference``: the same math with plain differentiable PyTorch ops (CPU tests, the fp32
+  parity oracle, and the "torch-eager" baseline).
+
+Covers every layer flavour the reference trains: post-LN BERT (HF BertLayer, SURVEY.md D15;
+reference model/bert_mp.py:22-24), pre-LN OPT/GPT-2/BLOOM blocks (D17) including causal
+masking and BLOOM ALiBi, and the instrumented OPT-style block of reference
+model/transformer.py:18-106 (see ``models/transformer_block.py`` for the hookable variant).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..ops import attention as A
+from ..ops import functional as Fx
+from ..ops.grad import emit_gemm_grad, grad_done, grad_dst, note_use
+from ..ops.rng import RngState
+from .config import TransformerConfig
+
+
+def init_linear_(w: torch.Tensor, b: torch.Tensor | None, std: float = 0.02) -> None:
+    with torch.no_grad():
+        w.normal_(0.0, std)
+        if b is not None:
+            b.zero_()
+
+
+class Runtime:
+    """Per-model execution settings shared by all submodules."""
+
+    def __init__(self, impl: str = "auto", rng: RngState | None = None, exact_dropout: bool = True):
+        self.impl = impl              # "auto" | "fused" | "reference"
+        self.rng = rng or RngState(seed=0)
+        self.exact_dropout = exact_dropout  # reference path uses the counter RNG masks
+        self._next_sid = 1
+
+    def new_sid(self) -> int:
+        """Dropout stream id for one call site; deterministic per model structure so two
+        builds of the same model (fused vs reference) draw identical masks."""
+        s = self._next_sid
+        self._next_sid += 1
+        return s
+
+    def use_fused(self, x: torch.Tensor) -> bool:
+        if self.impl == "fused":
+            return True
+        if self.impl == "reference":
+            return False
+        return x.is_cuda
+
+
+def ref_dropout(x, p, training, rt: Runtime, sid):
+    if not training or p <= 0:
+        return x
+    if rt.exact_dropout:
+        return Fx._ref_dropout(x, p, rt.rng, sid)
+    return F.dropout(x, p, True)
+
+
+class TransformerLayer(nn.Module):
+    def __init__(self, cfg: TransformerConfig, rt: Runtime):
+        super().__init__()
+        h, f = cfg.hidden_size, cfg.ffn_size
+        self.cfg, self.rt = cfg, rt
+        self.qkv_w = nn.Parameter(torch.empty(3 * h, h))
+        self.qkv_b = nn.Parameter(torch.zeros(3 * h))
+        self.o_w = nn.Parameter(torch.empty(h, h))
+        self.o_b = nn.Parameter(torch.zeros(h))
+        self.ln1_g = nn.Parameter(torch.ones(h))
+        self.ln1_b = nn.Parameter(torch.zeros(h))
+        self.fc1_w = nn.Parameter(torch.empty(f, h))
+        self.fc1_b = nn.Parameter(torch.zeros(f))
+        self.fc2_w = nn.Parameter(torch.empty(h, f))
+        self.fc2_b = nn.Parameter(torch.zeros(h))
+        self.ln2_g = nn.Parameter(torch.ones(h))
+        self.ln2_b = nn.Parameter(torch.zeros(h))
+        for w, b in ((self.qkv_w, self.qkv_b), (self.o_w, self.o_b), (self.fc1_w, self.fc1_b), (self.fc2_w, self.fc2_b)):
+            init_linear_(w, b)
+        self.sid_attn = rt.new_sid()
+        self.sid_1 = rt.new_sid()
+        self.sid_2 = rt.new_sid()
+        # ALiBi slopes stay fp32 (not a buffer, so model.to(bfloat16) does not round them).
+        self._alibi = A.alibi_slopes(cfg.num_heads) if cfg.alibi else None
+
+    @property
+    def alibi(self):
+        if self._alibi is None:
+            return None
+        dev = self.qkv_w.device
+        if self._alibi.device != dev:
+            self._alibi = self._alibi.to(dev)
+        return self._alibi
+
+    def params(self):
+        return (self.qkv_w, self.qkv_b, self.o_w, self.o_b, self.ln1_g, self.ln1_b,
+                self.fc1_w, self.fc1_b, self.fc2_w, self.fc2_b, self.ln2_g, self.ln2_b)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x: [B, S, h] -> [B, S, h]"""
+        if self.rt.use_fused(x):
+            note_use(self.params())
+            return _FusedLayerFn.apply(x, self, *self.params())
+        return self._reference(x)
+
+    # ------------------------------------------------------------------ reference path
+    def _reference(self, x: torch.Tensor) -> torch.Tensor:
+        c, rt = self.cfg, self.rt
+        B, S, h = x.shape
+        H, D = c.num_heads, c.head_dim
+        tr = self.training
+        p_h = c.hidden_dropout if tr else 0.0
+        p_a = c.attn_dropout if tr else 0.0
+
+        def attn(inp):
+            qkv = F.linear(inp, self.qkv_w, self.qkv_b).view(B, S, 3, H, D)
+            q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))
+            s = torch.matmul(q, k.transpose(-1, -2)) * (1.0 / math.sqrt(D))
+            if self.alibi is not None:
+                s = s + self.alibi.view(1, H, 1, 1).to(s.dtype) * torch.arange(S, device=s.device, dtype=s.dtype)
+            if c.causal:
+                s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+            prob = torch.softmax(s.float(), -1).to(s.dtype)
+            prob = ref_dropout(prob, p_a, tr, rt, rt.rng.sid(self.sid_attn))
+            ctx = torch.matmul(prob, v).transpose(1, 2).reshape(B, S, h)
+            return F.linear(ctx, self.o_w, self.o_b)
+
+        def mlp(inp):
+            u = F.linear(inp, self.fc1_w, self.fc1_b)
+            return F.linear(Fx._ref_act(u, c.activation) if c.activation != "gelu" else F.gelu(u), self.fc2_w, self.fc2_b)
+
+        ln = lambda t, g, b: F.layer_norm(t, (h,), g, b, c.ln_eps)
+        if c.pre_ln:
+            x = x + ref_dropout(attn(ln(x, self.ln1_g, self.ln1_b)), p_h, tr, rt, rt.rng.sid(self.sid_1))
+            x = x + ref_dropout(mlp(ln(x, self.ln2_g, self.ln2_b)), p_h, tr, rt, rt.rng.sid(self.sid_2))
+            return x
+        x = ln(x + ref_dropout(attn(x), p_h, tr, rt, rt.rng.sid(self.sid_1)), self.ln1_g, self.ln1_b)
+        x = ln(x + ref_dropout(mlp(x), p_h, tr, rt, rt.rng.sid(self.sid_2)), self.ln2_g, self.ln2_b)
+        return x
+
+
+def _acc(p):
+    return grad_dst(p)
+
+
+class _FusedLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, layer: TransformerLayer, *params):
+        c, rt = layer.cfg, layer.rt
+        (qkv_w, qkv_b, o_w, o_b, g1, b1, w1, bf1, w2, bf2, g2, b2) = params
+        B, S, h = x.shape
+        H, D = c.num_heads, c.head_dim
+        T = B * S
+        tr = layer.training
+        p_h = c.hidden_dropout if tr else 0.0
+        p_a = c.attn_dropout if tr else 0.0
+        rng = rt.rng
+        sa, s1, s2 = rng.sid(layer.sid_attn), rng.sid(layer.sid_1), rng.sid(layer.sid_2)
+        x2d = x.reshape(T, h)
+        eps = c.ln_eps
+        if c.pre_ln:
+            _, a_in, m1, r1 = Fx.ln_fwd(None, x2d, g1, b1, eps, 0.0, rng, 0)
+        else:
+            a_in = x2d
+        qkv = F.linear(a_in, qkv_w, qkv_b)
+        actx, lse = A.attn_fwd(qkv, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa)
+        o = F.linear(actx, o_w, o_b)
+        if c.pre_ln:
+            z1, f_in, m2, r2 = Fx.ln_fwd(o, x2d, g2, b2, eps, p_h, rng, s1)
+        else:
+            z1, f_in, m1, r1 = Fx.ln_fwd(o, x2d, g1, b1, eps, p_h, rng, s1)
+        u = F.linear(f_in, w1, bf1)
+        a = Fx.act_fwd(u, c.activation)
+        y = F.linear(a, w2, bf2)
+        if c.pre_ln:
+            out = z1 + Fx.dropout(y, p_h, rng, s2)
+            z2 = m3 = r3 = None
+        else:
+            z2, out, m3, r3 = Fx.ln_fwd(y, f_in, g2, b2, eps, p_h, rng, s2)
+        if c.pre_ln:
+            ctx.save_for_backward(x2d, a_in, qkv, actx, lse, z1, f_in, u, m1, r1, m2, r2)
+        else:
+            ctx.save_for_backward(x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3)
+        ctx.layer = layer
+        ctx.meta = (B, S, h, H, D, p_h, p_a, sa, s1, s2)
+        return out.view(B, S, h)
+
+    @staticmethod
+    def backward(ctx, dout):
+        layer = ctx.layer
+        c, rng = layer.cfg, layer.rt.rng
+        B, S, h, H, D, p_h, p_a, sa, s1, s2 = ctx.meta
+        T = B * S
+        (qkv_w, qkv_b, o_w, o_b, g1, b1, w1, bf1, w2, bf2, g2, b2) = layer.params()
+        dout = dout.reshape(T, h).contiguous()
+        if c.pre_ln:
+            x2d, a_in, qkv, actx, lse, z1, f_in, u, m1, r1, m2, r2 = ctx.saved_tensors
+            # out = z1 + dropout(y)
+            dy = Fx.dropout(dout, p_h, rng, s2)
+            Fx.bias_grad(dy, *_pair(bf2))
+            grad_done(bf2)
+        else:
+            x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3 = ctx.saved_tensors
+            # out = LN2(f_in + dropout(y)); dz2 = d(out)/d(z2), flows to f_in (residual) and y
+            dz2, dy = Fx.ln_bwd(dout, None, z2, m3, r3, g2, p_h, rng, s2, want_dz=True, want_dy=True,
+                                dgamma=_acc(g2), dbeta=_acc(b2), dbias=_acc(bf2))
+            for p in (g2, b2, bf2):
+                grad_done(p)
+        a = Fx.act_fwd(u, c.activation)
+        emit_gemm_grad(w2, dy.t(), a)
+        da = dy @ w2
+        du = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1))
+        grad_done(bf1)
+        emit_gemm_grad(w1, du.t(), f_in)
+        if c.pre_ln:
+            dfin = du @ w1
+            # z1 = x + dropout(o); f_in = LN2(z1); dz1 also receives dout (residual of out)
+            dz1, do = Fx.ln_bwd(dfin, dout, z1, m2, r2, g2, p_h, rng, s1, want_dz=True, want_dy=True,
+                                dgamma=_acc(g2), dbeta=_acc(b2), dbias=_acc(o_b))
+            for p in (g2, b2, o_b):
+                grad_done(p)
+        else:
+            # f_in = LN1(z1) feeds both the FFN and (as residual) z2
+            dfin = torch.addmm(dz2, du, w1)
+            dz1, do = Fx.ln_bwd(dfin, None, z1, m1, r1, g1, p_h, rng, s1, want_dz=True, want_dy=True,
+                                dgamma=_acc(g1), dbeta=_acc(b1), dbias=_acc(o_b))
+            for p in (g1, b1, o_b):
+                grad_done(p)
+        emit_gemm_grad(o_w, do.t(), actx)
+        dctx = do @ o_w
+        dqkv = A.attn_bwd(dctx, qkv, actx, lse, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa)
+        Fx.bias_grad(dqkv, *_pair(qkv_b))
+        grad_done(qkv_b)
+        if c.pre_ln:
+            emit_gemm_grad(qkv_w, dqkv.t(), a_in)
+            dain = dqkv @ qkv_w
+            dx, _ = Fx.ln_bwd(dain, dz1, x2d, m1, r1, g1, 0.0, rng, 0, want_dz=True, want_dy=False,
+                              dgamma=_acc(g1), dbeta=_acc(b1))
+            for p in (g1, b1):
+                grad_done(p)
+        else:
+            emit_gemm_grad(qkv_w, dqkv.t(), x2d)
+            dx = torch.addmm(dz1, dqkv, qkv_w)
+        return (dx.view(B, S, h), None) + (None,) * 12
+
+
+def _pair(p):
+    dst, acc = grad_dst(p)
+    return dst, acc

@@ -1,0 +1,118 @@
+"""ctypes binding of the in-tree gfx950 kernel library ``ops/_dtd_kernels.so``.
+
+The library exposes a C ABI (``extern "C" int dtd_*(..., hipStream_t)``); every launch goes
+onto torch's *current* HIP stream, so kernels interleave correctly with hipBLASLt GEMMs and
+RCCL collectives issued by torch, and are captured by ``torch.cuda.graph`` like any ATen op.
+
+On a machine with a GPU the library is REQUIRED: ``lib()`` raises if it cannot be built or
+loaded (no silent fallback to eager PyTorch on the GPU path).  On CPU-only hosts the pure
+PyTorch reference implementations in ``ops/ref.py`` are used instead.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be imported first: binds libamdhip64 to torch's runtime)
+
+from . import build as _build
+
+_LIB = None
+_LOCK = threading.Lock()
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+F = ctypes.c_float
+SZ = ctypes.c_size_t
+U32 = ctypes.c_uint32
+
+_SIGS = {
+    # norm.hip
+    "dtd_ln_bwd_num_partials": (I, [I, I]),
+    "dtd_ln_fwd": (I, [I, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, P]),
+    "dtd_ln_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, F, P, U32, P]),
+    # act.hip
+    "dtd_act_fwd": (I, [I, P, P, SZ, I, P]),
+    "dtd_act_bwd_num_partials": (I, [I, I]),
+    "dtd_act_bwd": (I, [I, P, P, P, P, I, I, I, P]),
+    "dtd_colsum_finalize": (I, [P, I, I, P, I, I, F, P]),
+    # xent.hip
+    "dtd_xent_fwd": (I, [I, P, P, P, P, P, I, I, I, P]),
+    "dtd_xent_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P]),
+    # embed.hip
+    "dtd_embed_fwd": (I, [I, P, P, P, P, P, P, I, I, I, I, P]),
+    "dtd_embed_word_bwd": (I, [I, I, P, P, P, P, I, I, I, I, P]),
+    "dtd_embed_pos_bwd": (I, [I, I, P, P, I, I, I, I, I, P]),
+    "dtd_dropout": (I, [I, P, P, SZ, F, P, U32, P]),
+    # adam.hip
+    "dtd_adam_step": (I, [P, P, P, P, I, P, SZ, P, I, P]),
+    "dtd_scale_cast": (I, [P, I, P, I, SZ, F, P, P]),
+    "dtd_sqnorm_num_partials": (I, [SZ]),
+    "dtd_sqnorm_partials": (I, [P, I, SZ, P, P]),
+    # attention.hip
+    "dtd_attn_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, F, F, P, U32, P]),
+    "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, F, F, P, U32, P]),
+}
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def available() -> bool:
+    """True when a GPU is present (the HIP library is then mandatory)."""
+    return torch.cuda.is_available()
+
+
+def lib():
+    """Load (building first if stale) the kernel library. Raises on failure."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = _build.LIB_PATH
+        if os.environ.get("DTD_NO_BUILD") != "1" and _build.needs_build():
+            _build.build(verbose=True)
+        if not path.exists():
+            raise KernelError(f"HIP kernel library missing: {path} (run ops/build.py)")
+        so = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(so, name, None)
+            if fn is None:
+                continue  # optional kernels (e.g. attention while under development)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = so
+        return _LIB
+
+
+def has(name: str) -> bool:
+    return hasattr(lib(), name)
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise KernelError(f"{name} failed with hipError {rc}")
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+DT_F32, DT_BF16 = 0, 1
+
+
+def dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return DT_BF16
+    if t.dtype == torch.float32:
+        return DT_F32
+    raise TypeError(f"unsupported dtype {t.dtype} (kernels take bf16 or fp32)")

@@ -1,0 +1,146 @@
+"""Scaled-dot-product attention core: flash-style HIP kernels (gfx950 MFMA) + math reference.
+
+Layout contract (shared by kernels, reference and models): the fused projection output
+``qkv`` is ``[B*S, 3*H*D]`` viewed as ``[B, S, 3, H, D]`` (q, k, v blocks), the context
+output ``ctx`` is ``[B*S, H*D]`` and the log-sum-exp ``lse`` is ``[B, H, S]`` fp32 (natural
+log of sum(exp(score)), score = q.k * scale + bias).  Supported score modifiers: causal mask,
+ALiBi (BLOOM: bias = slope_h * key_position, which equals BLOOM's relative form up to a
+per-row constant that softmax cancels) and dropout on the probabilities with the counter RNG
+(mask element index = ((b*H + h)*S + i)*S + j, regenerated in backward).
+
+Reference semantics: HF BertSelfAttention eager path (matmul, softmax, dropout, matmul --
+SURVEY.md K2, reference model/transformer.py:80-86); the reference never passes an
+attention mask for BERT (data_parallel_training.py:53), so padding is attended to.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+from .rng import RngState, keep_mask
+
+
+def alibi_slopes(num_heads: int) -> torch.Tensor:
+    """BLOOM/ALiBi head slopes (geometric sequence, with the interleaved extension for
+    non-power-of-two head counts)."""
+    def pow2(n):
+        start = 2 ** (-(2 ** -(math.log2(n) - 3)))
+        return [start * (start ** i) for i in range(n)]
+    if math.log2(num_heads).is_integer():
+        s = pow2(num_heads)
+    else:
+        c = 2 ** math.floor(math.log2(num_heads))
+        s = pow2(c) + pow2(2 * c)[0::2][: num_heads - c]
+    return torch.tensor(s, dtype=torch.float32)
+
+
+def _split(qkv, B, S, H, D):
+    x = qkv.view(B, S, 3, H, D)
+    return x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+
+
+def _scores(q, k, scale, causal, slopes):
+    s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
+    S = q.shape[2]
+    if slopes is not None:
+        s = s + slopes.to(s.device).view(1, -1, 1, 1) * torch.arange(S, device=s.device, dtype=s.dtype).view(1, 1, 1, S)
+    if causal:
+        m = torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1)
+        s = s.masked_fill(m, float("-inf"))
+    return s
+
+
+def _drop_mask(B, H, S, p, rng, sid, device):
+    seed, step = (int(v) for v in rng.state.tolist())
+    return keep_mask(B * H * S * S, p, seed, step, sid, device=device).view(B, H, S, S)
+
+
+def attn_fwd_ref(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | None = None, sid=0,
+                 scale=None):
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    q, k, v = _split(qkv, B, S, H, D)
+    s = _scores(q, k, scale, causal, slopes)
+    lse = torch.logsumexp(s, -1)
+    prob = torch.exp(s - lse[..., None])
+    if p > 0:
+        prob = prob * _drop_mask(B, H, S, p, rng, sid, qkv.device) / (1.0 - p)
+    ctx = torch.matmul(prob, v.float())  # [B,H,S,D]
+    return ctx.transpose(1, 2).reshape(B * S, H * D).to(qkv.dtype), lse
+
+
+def attn_bwd_ref(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, rng=None, sid=0, scale=None):
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    q, k, v = _split(qkv, B, S, H, D)
+    s = _scores(q, k, scale, causal, slopes)
+    prob = torch.exp(s - lse[..., None])
+    do = dctx.view(B, S, H, D).transpose(1, 2).float()
+    o = ctx.view(B, S, H, D).transpose(1, 2).float()
+    if p > 0:
+        keep = _drop_mask(B, H, S, p, rng, sid, qkv.device).float() / (1.0 - p)
+        pd = prob * keep
+    else:
+        keep, pd = None, prob
+    dv = torch.matmul(pd.transpose(-1, -2), do)
+    dpd = torch.matmul(do, v.float().transpose(-1, -2))
+    dp = dpd * keep if keep is not None else dpd
+    delta = (do * o).sum(-1, keepdim=True)
+    ds = prob * (dp - delta)
+    dq = torch.matmul(ds, k.float()) * scale
+    dk = torch.matmul(ds.transpose(-1, -2), q.float()) * scale
+    dqkv = torch.stack([dq, dk, dv], dim=2)  # [B,H,3,S,D]
+    return dqkv.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * H * D).to(qkv.dtype)
+
+
+_WARNED = []
+
+
+def _warn_once():
+    if not _WARNED:
+        import warnings
+        warnings.warn("HIP flash-attention kernel not built: using the math reference on GPU")
+        _WARNED.append(1)
+
+
+def kernel_supported(qkv: torch.Tensor, D: int) -> bool:
+    return qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128) and _lib.has("dtd_attn_fwd")
+
+
+def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | None = None, sid=0):
+    """Returns (ctx [B*S, H*D], lse [B, H, S] fp32)."""
+    if not kernel_supported(qkv, D):
+        if qkv.is_cuda and qkv.dtype == torch.bfloat16 and _lib.has("dtd_attn_fwd") is False:
+            _warn_once()
+        return attn_fwd_ref(qkv, B, S, H, D, causal, slopes, p, rng, sid)
+    qkv = qkv.contiguous()
+    ctx = torch.empty((B * S, H * D), dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+    sl = slopes.to(device=qkv.device, dtype=torch.float32).contiguous() if slopes is not None else None
+    # q/k/v are strided views into qkv: row stride 3*H*D, head stride D.
+    ld = 3 * H * D
+    base = qkv.data_ptr()
+    es = qkv.element_size()
+    _lib.call("dtd_attn_fwd", base, base + H * D * es, base + 2 * H * D * es, ctx.data_ptr(), lse.data_ptr(),
+              _lib.ptr(sl), B, S, H, D, ld, H * D, int(causal), 0, 0, 1.0 / math.sqrt(D), float(p),
+              rng.state.data_ptr() if rng is not None else None, sid, _lib.stream())
+    return ctx, lse
+
+
+def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, rng=None, sid=0):
+    """Returns dqkv [B*S, 3*H*D] in the qkv layout."""
+    if not kernel_supported(qkv, D):
+        return attn_bwd_ref(dctx, qkv, ctx, lse, B, S, H, D, causal, slopes, p, rng, sid)
+    dctx = dctx.contiguous()
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+    dq_acc = torch.zeros((B, H, S, D), dtype=torch.float32, device=qkv.device)
+    sl = slopes.to(device=qkv.device, dtype=torch.float32).contiguous() if slopes is not None else None
+    ld = 3 * H * D
+    es = qkv.element_size()
+    qb, gb = qkv.data_ptr(), dqkv.data_ptr()
+    _lib.call("dtd_attn_bwd", qb, qb + H * D * es, qb + 2 * H * D * es, ctx.data_ptr(), dctx.data_ptr(),
+              lse.data_ptr(), delta.data_ptr(), dq_acc.data_ptr(), gb, gb + H * D * es, gb + 2 * H * D * es,
+              _lib.ptr(sl), B, S, H, D, ld, H * D, int(causal), 0, 0, 1.0 / math.sqrt(D), float(p),
+              rng.state.data_ptr() if rng is not None else None, sid, _lib.stream())
+    return dqkv

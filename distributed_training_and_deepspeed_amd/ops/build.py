@@ -1,0 +1,95 @@
+"""In-tree build of the gfx950 HIP kernel library (``ops/_dtd_kernels.so``).
+
+Every ``ops/csrc/*.hip`` file is compiled with ``hipcc --offload-arch=gfx950`` into an object
+and linked into one shared library that exports a plain C ABI (``extern "C" dtd_*``).
+Python binds it with ctypes (``ops/_lib.py``) after ``import torch`` so the library resolves
+``libamdhip64.so.7`` to the HIP runtime torch already loaded (one HIP runtime per process).
+
+The library is rebuilt only when a source or header is newer than it.  Run directly:
+``python -m distributed_training_and_deepspeed_amd.ops.build [--force] [-j N]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+LIB_NAME = "_dtd_kernels.so"
+LIB_PATH = HERE / LIB_NAME
+OBJ_DIR = HERE / "build"
+ARCH = os.environ.get("DTD_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC or install ROCm)")
+
+
+def sources() -> list[Path]:
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _headers() -> list[Path]:
+    return sorted(CSRC.glob("*.h"))
+
+
+def needs_build() -> bool:
+    if not LIB_PATH.exists():
+        return True
+    t = LIB_PATH.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in sources() + _headers() + [Path(__file__)])
+
+
+def _compile(src: Path, hipcc: str, extra: list[str]) -> Path:
+    OBJ_DIR.mkdir(exist_ok=True)
+    obj = OBJ_DIR / (src.stem + ".o")
+    hdr_t = max((p.stat().st_mtime for p in _headers()), default=0)
+    if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, hdr_t, Path(__file__).stat().st_mtime):
+        return obj
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", str(src), "-o", str(obj),
+           "-I", str(CSRC), "-Wno-unused-command-line-argument", "-fvisibility=hidden", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
+    """Compile all kernels for gfx950 and link ``_dtd_kernels.so`` in-tree; return its path."""
+    if not force and not needs_build():
+        return LIB_PATH
+    hipcc = _hipcc()
+    extra = os.environ.get("DTD_HIPCC_FLAGS", "").split()
+    srcs = sources()
+    if force and OBJ_DIR.exists():
+        shutil.rmtree(OBJ_DIR)
+    jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
+    if verbose:
+        print(f"[dtd.build] compiling {len(srcs)} HIP sources for {ARCH} with {jobs} jobs", file=sys.stderr)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hipcc, extra), srcs))
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB_PATH)
+    if verbose:
+        print(f"[dtd.build] wrote {LIB_PATH}", file=sys.stderr)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args()
+    build(force=a.force, jobs=a.jobs)

@@ -1,0 +1,154 @@
+// Activation (GELU-erf / GELU-tanh / ReLU) forward and backward with fused bias-gradient
+// column partials, plus the deterministic column-sum finaliser used by every kernel that
+// produces parameter-gradient partials (LayerNorm gamma/beta, Linear biases).
+//
+// Reference ops replaced: HF BertIntermediate `gelu` (erf), BLOOM/GPT-2 tanh-GELU, OPT/
+// TransformerBlock ReLU (reference model/transformer.py:52,101) and the implicit
+// `bias.grad = dY.sum(0)` reductions of every nn.Linear (SURVEY.md K5, K1 epilogues).
+// The Linear bias itself is added by the hipBLASLt epilogue of the producing GEMM, so the
+// forward here is a pure elementwise pass over the pre-activation `u`.
+#include "common.h"
+
+using namespace dtd;
+
+namespace {
+
+enum Act : int { kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3 };
+
+__device__ __forceinline__ float act_f(int act, float x) {
+  switch (act) {
+    case kGeluErf: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case kGeluTanh: {
+      const float k = 0.7978845608028654f;
+      return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
+    }
+    case kRelu: return x > 0.f ? x : 0.f;
+    default: return x;
+  }
+}
+__device__ __forceinline__ float act_df(int act, float x) {
+  switch (act) {
+    case kGeluErf: {
+      const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+      const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+      return cdf + x * pdf;
+    }
+    case kGeluTanh: {
+      const float k = 0.7978845608028654f;
+      const float t = tanhf(k * (x + 0.044715f * x * x * x));
+      return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+    }
+    case kRelu: return x > 0.f ? 1.f : 0.f;
+    default: return 1.f;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ u, T* __restrict__ y, size_t n, int act) {
+  const size_t nv = n / 8;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
+    float t[8];
+    vload<T, 8>(u + i * 8, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = act_f(act, t[j]);
+    vstore<T, 8>(y + i * 8, t);
+  }
+  // tail (n % 8) handled by block 0
+  if (blockIdx.x == 0) {
+    for (size_t i = nv * 8 + threadIdx.x; i < n; i += blockDim.x) y[i] = (T)act_f(act, (float)u[i]);
+  }
+}
+
+// du = dy * act'(u) (act == kNone: du = dy), column partials of du per row-group.
+// grid = (col_tiles, row_groups); block = 128 threads x 8 columns = 1024-column tile.
+template <typename T>
+__global__ void __launch_bounds__(128) act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ u,
+                                                      T* __restrict__ du, float* __restrict__ part,
+                                                      int rows, int cols, int act) {
+  const int col = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (col >= cols) return;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int r = blockIdx.y; r < rows; r += gridDim.y) {
+    const size_t off = (size_t)r * cols + col;
+    float d[8];
+    vload<T, 8>(dy + off, d);
+    if (act != kNone) {
+      float x[8];
+      vload<T, 8>(u + off, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] *= act_df(act, x[j]);
+    }
+    if (du) vstore<T, 8>(du + off, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += d[j];
+  }
+  if (part) vstore<float, 8>(part + (size_t)blockIdx.y * cols + col, acc);
+}
+
+// out[c] = (accumulate ? out[c] : 0) + sum_p part[p][c]; fixed summation order.
+// block = 256 threads = 64 columns x 4 part-slices, combined through LDS.
+template <typename O>
+__global__ void __launch_bounds__(256) colsum_finalize_kernel(const float* __restrict__ part, int nparts, int cols,
+                                                              O* __restrict__ out, int accumulate, float scale) {
+  __shared__ float sh[4][64];
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  float t = 0.f;
+  if (col < cols) {
+    for (int p = sl; p < nparts; p += 4) t += part[(size_t)p * cols + col];
+  }
+  sh[sl][lane] = t;
+  __syncthreads();
+  if (sl == 0 && col < cols) {
+    float s = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
+    s *= scale;
+    if (accumulate) s += (float)out[col];
+    out[col] = (O)s;
+  }
+}
+
+}  // namespace
+
+DTD_EXPORT int dtd_act_fwd(int dtype, const void* u, void* y, size_t n, int act, hipStream_t s) {
+  if (n == 0) return 0;
+  size_t blocks = (n / 8 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  if (dtype == kBF16) hipLaunchKernelGGL(act_fwd_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)u, (bf16*)y, n, act);
+  else hipLaunchKernelGGL(act_fwd_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)u, (float*)y, n, act);
+  DTD_LAUNCH_CHECK();
+}
+
+// Row groups used by dtd_act_bwd for a [rows, cols] operand (callers size `part` [n, cols]).
+DTD_EXPORT int dtd_act_bwd_num_partials(int rows, int cols) {
+  const int tiles = (cols + 1023) / 1024;
+  int g = 1024 / tiles;
+  if (g < 1) g = 1;
+  if (g > rows) g = rows;
+  return g;
+}
+
+DTD_EXPORT int dtd_act_bwd(int dtype, const void* dy, const void* u, void* du, float* part, int rows, int cols,
+                           int act, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (cols % 8) return (int)hipErrorInvalidValue;
+  dim3 grid((cols + 1023) / 1024, dtd_act_bwd_num_partials(rows, cols));
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(act_bwd_kernel<bf16>, grid, dim3(128), 0, s, (const bf16*)dy, (const bf16*)u, (bf16*)du, part, rows, cols, act);
+  else
+    hipLaunchKernelGGL(act_bwd_kernel<float>, grid, dim3(128), 0, s, (const float*)dy, (const float*)u, (float*)du, part, rows, cols, act);
+  DTD_LAUNCH_CHECK();
+}
+
+DTD_EXPORT int dtd_colsum_finalize(const float* part, int nparts, int cols, void* out, int out_dtype, int accumulate,
+                                   float scale, hipStream_t s) {
+  if (cols <= 0) return 0;
+  dim3 grid((cols + 63) / 64);
+  if (out_dtype == kBF16)
+    hipLaunchKernelGGL(colsum_finalize_kernel<bf16>, grid, dim3(256), 0, s, part, nparts, cols, (bf16*)out, accumulate, scale);
+  else
+    hipLaunchKernelGGL(colsum_finalize_kernel<float>, grid, dim3(256), 0, s, part, nparts, cols, (float*)out, accumulate, scale);
+  DTD_LAUNCH_CHECK();
+}

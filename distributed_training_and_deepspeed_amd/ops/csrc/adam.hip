@@ -1,0 +1,154 @@
+// Fused Adam / AdamW step over flat parameter buffers, plus the flat-buffer utility kernels
+// (scale+cast for gradient buckets, squared L2 norm partials for clipping).
+//
+// Replaces DeepSpeed FusedAdam (`multi_tensor_adam.cu`, selected by zero_dp_training.py:28-33),
+// torch AdamW foreach kernels (model_parallel_training.py:50) and the per-parameter Python loop
+// of transformers.AdamW (data_parallel_training.py:34) -- SURVEY.md D12/D21/K9.
+//
+// The framework keeps parameters, fp32 master weights, moments and gradients in flat buffers,
+// so one launch updates the whole model (or the local ZeRO partition): 16 B per lane per
+// stream, HBM-bound at ~28 B/param.  Hyper-parameters are read from a small device array so
+// a hipGraph replay sees the current step (bias correction) and a device-computed gradient
+// scale (1/world, clipping) without host round trips:
+//   hp[0] lr   hp[1] beta1   hp[2] beta2   hp[3] eps   hp[4] weight_decay
+//   hp[5] step (already incremented for this update)   hp[6] grad scale
+// mode bits: 1 = decoupled weight decay (AdamW; else L2 added to the gradient),
+//            2 = bias correction,
+//            4 = HF transformers eps placement: p -= lr*sqrt(bc2)/bc1 * m / (sqrt(v) + eps)
+//                (torch / DeepSpeed: p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)).
+#include "common.h"
+
+using namespace dtd;
+
+namespace {
+
+struct AdamArgs {
+  float* p; float* m; float* v; const void* g; bf16* p_lp; size_t n; const float* hp; int mode; int g_dtype;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float lr, float b1, float b2,
+                                          float eps, float wd, float bc1, float bc2_sqrt, int mode) {
+  if (!(mode & 1) && wd != 0.f) g += wd * p;
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  if (mode & 1) p -= lr * wd * p;
+  if (mode & 4) {
+    const float step = lr * bc2_sqrt / bc1;
+    p -= step * m / (sqrtf(v) + eps);
+  } else {
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p -= (lr / bc1) * m / denom;
+  }
+}
+
+__global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
+  const float lr = a.hp[0], b1 = a.hp[1], b2 = a.hp[2], eps = a.hp[3], wd = a.hp[4];
+  const float step = a.hp[5], gs = a.hp[6];
+  float bc1 = 1.f, bc2s = 1.f;
+  if (a.mode & 2) {
+    bc1 = 1.f - powf(b1, step);
+    bc2s = sqrtf(1.f - powf(b2, step));
+  }
+  const size_t nv = a.n / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
+    float4 p = reinterpret_cast<float4*>(a.p)[i];
+    float4 m = reinterpret_cast<float4*>(a.m)[i];
+    float4 v = reinterpret_cast<float4*>(a.v)[i];
+    float g[4];
+    if (a.g_dtype == kBF16) vload<bf16, 4>((const bf16*)a.g + i * 4, g);
+    else vload<float, 4>((const float*)a.g + i * 4, g);
+    adam_elem(p.x, m.x, v.x, g[0] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
+    adam_elem(p.y, m.y, v.y, g[1] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
+    adam_elem(p.z, m.z, v.z, g[2] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
+    adam_elem(p.w, m.w, v.w, g[3] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
+    reinterpret_cast<float4*>(a.p)[i] = p;
+    reinterpret_cast<float4*>(a.m)[i] = m;
+    reinterpret_cast<float4*>(a.v)[i] = v;
+    if (a.p_lp) {
+      const float q[4] = {p.x, p.y, p.z, p.w};
+      vstore<bf16, 4>(a.p_lp + i * 4, q);
+    }
+  }
+  if (blockIdx.x == 0) {
+    for (size_t e = nv * 4 + threadIdx.x; e < a.n; e += blockDim.x) {
+      float g = a.g_dtype == kBF16 ? (float)((const bf16*)a.g)[e] : ((const float*)a.g)[e];
+      adam_elem(a.p[e], a.m[e], a.v[e], g * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
+      if (a.p_lp) a.p_lp[e] = (bf16)a.p[e];
+    }
+  }
+}
+
+template <typename S, typename D>
+__global__ void __launch_bounds__(256) scale_cast_kernel(const S* __restrict__ src, D* __restrict__ dst, size_t n,
+                                                         float scale, const float* __restrict__ dscale) {
+  const float sc = dscale ? scale * dscale[0] : scale;
+  const size_t nv = n / 8;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
+    float t[8];
+    vload<S, 8>(src + i * 8, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] *= sc;
+    vstore<D, 8>(dst + i * 8, t);
+  }
+  if (blockIdx.x == 0)
+    for (size_t e = nv * 8 + threadIdx.x; e < n; e += blockDim.x) dst[e] = (D)((float)src[e] * sc);
+}
+
+// Per-block partial sums of x^2 (fp32), written to part[blockIdx.x].
+template <typename S>
+__global__ void __launch_bounds__(256) sqnorm_kernel(const S* __restrict__ x, size_t n, float* __restrict__ part) {
+  __shared__ float sh[8];
+  float acc = 0.f;
+  const size_t nv = n / 8;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
+    float t[8];
+    vload<S, 8>(x + i * 8, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += t[j] * t[j];
+  }
+  if (blockIdx.x == 0)
+    for (size_t e = nv * 8 + threadIdx.x; e < n; e += blockDim.x) { float t = (float)x[e]; acc += t * t; }
+  acc = block_sum(acc, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+size_t grid_for(size_t nvec) {
+  size_t b = (nvec + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;
+  return b;
+}
+
+}  // namespace
+
+DTD_EXPORT int dtd_adam_step(float* p, float* m, float* v, const void* g, int g_dtype, void* p_lp, size_t n,
+                             const float* hp, int mode, hipStream_t s) {
+  if (n == 0) return 0;
+  AdamArgs a{p, m, v, g, (bf16*)p_lp, n, hp, mode, g_dtype};
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, a);
+  DTD_LAUNCH_CHECK();
+}
+
+DTD_EXPORT int dtd_scale_cast(const void* src, int src_dtype, void* dst, int dst_dtype, size_t n, float scale,
+                              const float* dscale, hipStream_t s) {
+  if (n == 0) return 0;
+  dim3 grid(grid_for(n / 8));
+  if (src_dtype == kBF16 && dst_dtype == kBF16)
+    hipLaunchKernelGGL((scale_cast_kernel<bf16, bf16>), grid, dim3(256), 0, s, (const bf16*)src, (bf16*)dst, n, scale, dscale);
+  else if (src_dtype == kBF16)
+    hipLaunchKernelGGL((scale_cast_kernel<bf16, float>), grid, dim3(256), 0, s, (const bf16*)src, (float*)dst, n, scale, dscale);
+  else if (dst_dtype == kBF16)
+    hipLaunchKernelGGL((scale_cast_kernel<float, bf16>), grid, dim3(256), 0, s, (const float*)src, (bf16*)dst, n, scale, dscale);
+  else
+    hipLaunchKernelGGL((scale_cast_kernel<float, float>), grid, dim3(256), 0, s, (const float*)src, (float*)dst, n, scale, dscale);
+  DTD_LAUNCH_CHECK();
+}
+
+DTD_EXPORT int dtd_sqnorm_num_partials(size_t n) { return (int)grid_for(n / 8); }
+
+DTD_EXPORT int dtd_sqnorm_partials(const void* x, int dtype, size_t n, float* part, hipStream_t s) {
+  dim3 grid(grid_for(n / 8));
+  if (dtype == kBF16) hipLaunchKernelGGL(sqnorm_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, n, part);
+  else hipLaunchKernelGGL(sqnorm_kernel<float>, grid, dim3(256), 0, s, (const float*)x, n, part);
+  DTD_LAUNCH_CHECK();
+}

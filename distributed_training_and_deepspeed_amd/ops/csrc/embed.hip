@@ -1,0 +1,171 @@
+// Embedding gather-sum forward and deterministic scatter backward, plus standalone dropout.
+//
+// Reference ops replaced: HF BertEmbeddings (word + position + token-type -> LN -> dropout),
+// GPT-2 wte+wpe, OPT embed_tokens + learned positions (offset 2), BLOOM word embeddings
+// (SURVEY.md K7).  The LayerNorm is the shared norm kernel; dropout after the LN is
+// `dtd_dropout` below (mask regenerated in backward from the counter RNG).
+//
+// Backward of the word table (up to 250,880 x 1024 for BLOOM) is a *sorted segment sum*:
+// token ids are sorted once (on device), and each run of equal ids is summed in fp32 by one
+// workgroup that owns that table row exclusively, so there are no float atomics and the
+// result is bitwise reproducible (cdna_hip_programming.md Appendix B "Scatter / gather").
+#include "common.h"
+
+using namespace dtd;
+
+namespace {
+
+struct GatherArgs {
+  const int64_t* ids; const int64_t* type_ids;
+  const void* word; const void* pos; const void* type;
+  void* out; int rows, h, seq, pos_offset;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) embed_fwd_kernel(GatherArgs a) {
+  const int row = blockIdx.x;
+  const int64_t id = a.ids[row];
+  const int pidx = (row % a.seq) + a.pos_offset;
+  const int64_t tid = a.type_ids ? a.type_ids[row] : 0;
+  const T* w = (const T*)a.word + (size_t)id * a.h;
+  const T* p = a.pos ? (const T*)a.pos + (size_t)pidx * a.h : nullptr;
+  const T* t = a.type ? (const T*)a.type + (size_t)tid * a.h : nullptr;
+  T* o = (T*)a.out + (size_t)row * a.h;
+  for (int c = threadIdx.x * 2; c < a.h; c += blockDim.x * 2) {
+    float x[2], y[2];
+    vload<T, 2>(w + c, x);
+    if (p) { vload<T, 2>(p + c, y); x[0] += y[0]; x[1] += y[1]; }
+    if (t) { vload<T, 2>(t + c, y); x[0] += y[0]; x[1] += y[1]; }
+    vstore<T, 2>(o + c, x);
+  }
+}
+
+// One block per sorted position; only the first position of each run of equal ids works.
+template <typename T, typename G>
+__global__ void __launch_bounds__(256) embed_word_bwd_kernel(const int64_t* __restrict__ sorted_ids,
+                                                             const int64_t* __restrict__ perm,
+                                                             const T* __restrict__ dz, G* __restrict__ grad,
+                                                             int rows, int h, int accumulate, int padding_idx) {
+  const int i = blockIdx.x;
+  const int64_t id = sorted_ids[i];
+  if (i > 0 && sorted_ids[i - 1] == id) return;
+  if (id == padding_idx) return;
+  int j = i + 1;
+  while (j < rows && sorted_ids[j] == id) ++j;
+  G* g = grad + (size_t)id * h;
+  for (int c = threadIdx.x * 2; c < h; c += blockDim.x * 2) {
+    float acc[2] = {0.f, 0.f};
+    for (int k = i; k < j; ++k) {
+      float x[2];
+      vload<T, 2>(dz + (size_t)perm[k] * h + c, x);
+      acc[0] += x[0]; acc[1] += x[1];
+    }
+    if (accumulate) {
+      float old[2];
+      vload<G, 2>(g + c, old);
+      acc[0] += old[0]; acc[1] += old[1];
+    }
+    vstore<G, 2>(g + c, acc);
+  }
+}
+
+// grad_pos[s + offset] (+)= sum_b dz[b*seq + s]; grid = seq rows.
+template <typename T, typename G>
+__global__ void __launch_bounds__(256) embed_pos_bwd_kernel(const T* __restrict__ dz, G* __restrict__ grad, int batch,
+                                                            int seq, int h, int pos_offset, int accumulate) {
+  const int s = blockIdx.x;
+  G* g = grad + (size_t)(s + pos_offset) * h;
+  for (int c = threadIdx.x * 2; c < h; c += blockDim.x * 2) {
+    float acc[2] = {0.f, 0.f};
+    for (int b = 0; b < batch; ++b) {
+      float x[2];
+      vload<T, 2>(dz + ((size_t)b * seq + s) * h + c, x);
+      acc[0] += x[0]; acc[1] += x[1];
+    }
+    if (accumulate) {
+      float old[2];
+      vload<G, 2>(g + c, old);
+      acc[0] += old[0]; acc[1] += old[1];
+    }
+    vstore<G, 2>(g + c, acc);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_kernel(const T* __restrict__ x, T* __restrict__ y, size_t n, float p,
+                                                      const uint64_t* rng, uint32_t stream_id) {
+  DropoutRng g(rng, stream_id);
+  const uint32_t thr = keep_threshold(p);
+  const float scale = 1.f / (1.f - p);
+  const size_t nv = n / 8;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
+    float t[8];
+    vload<T, 8>(x + i * 8, t);
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const uint32_t b = g.bits((i * 8 + j) >> 1);
+      t[j] *= ((b & 0xffffu) >= thr) ? scale : 0.f;
+      t[j + 1] *= ((b >> 16) >= thr) ? scale : 0.f;
+    }
+    vstore<T, 8>(y + i * 8, t);
+  }
+  if (blockIdx.x == 0) {
+    for (size_t e = nv * 8 + threadIdx.x; e < n; e += blockDim.x) {
+      const uint32_t b = g.bits(e >> 1);
+      const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
+      y[e] = (T)((float)x[e] * (h16 >= thr ? scale : 0.f));
+    }
+  }
+}
+
+}  // namespace
+
+DTD_EXPORT int dtd_embed_fwd(int dtype, const int64_t* ids, const int64_t* type_ids, const void* word, const void* pos,
+                             const void* type, void* out, int rows, int h, int seq, int pos_offset, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (h % 2) return (int)hipErrorInvalidValue;
+  GatherArgs a{ids, type_ids, word, pos, type, out, rows, h, seq, pos_offset};
+  if (dtype == kBF16) hipLaunchKernelGGL(embed_fwd_kernel<bf16>, dim3(rows), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(embed_fwd_kernel<float>, dim3(rows), dim3(256), 0, s, a);
+  DTD_LAUNCH_CHECK();
+}
+
+DTD_EXPORT int dtd_embed_word_bwd(int dtype, int grad_dtype, const int64_t* sorted_ids, const int64_t* perm,
+                                  const void* dz, void* grad, int rows, int h, int accumulate, int padding_idx,
+                                  hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (dtype == kBF16 && grad_dtype == kBF16)
+    hipLaunchKernelGGL((embed_word_bwd_kernel<bf16, bf16>), dim3(rows), dim3(256), 0, s, sorted_ids, perm, (const bf16*)dz, (bf16*)grad, rows, h, accumulate, padding_idx);
+  else if (dtype == kBF16)
+    hipLaunchKernelGGL((embed_word_bwd_kernel<bf16, float>), dim3(rows), dim3(256), 0, s, sorted_ids, perm, (const bf16*)dz, (float*)grad, rows, h, accumulate, padding_idx);
+  else if (grad_dtype == kBF16)
+    hipLaunchKernelGGL((embed_word_bwd_kernel<float, bf16>), dim3(rows), dim3(256), 0, s, sorted_ids, perm, (const float*)dz, (bf16*)grad, rows, h, accumulate, padding_idx);
+  else
+    hipLaunchKernelGGL((embed_word_bwd_kernel<float, float>), dim3(rows), dim3(256), 0, s, sorted_ids, perm, (const float*)dz, (float*)grad, rows, h, accumulate, padding_idx);
+  DTD_LAUNCH_CHECK();
+}
+
+DTD_EXPORT int dtd_embed_pos_bwd(int dtype, int grad_dtype, const void* dz, void* grad, int batch, int seq, int h,
+                                 int pos_offset, int accumulate, hipStream_t s) {
+  if (batch <= 0) return 0;
+  if (dtype == kBF16 && grad_dtype == kBF16)
+    hipLaunchKernelGGL((embed_pos_bwd_kernel<bf16, bf16>), dim3(seq), dim3(256), 0, s, (const bf16*)dz, (bf16*)grad, batch, seq, h, pos_offset, accumulate);
+  else if (dtype == kBF16)
+    hipLaunchKernelGGL((embed_pos_bwd_kernel<bf16, float>), dim3(seq), dim3(256), 0, s, (const bf16*)dz, (float*)grad, batch, seq, h, pos_offset, accumulate);
+  else if (grad_dtype == kBF16)
+    hipLaunchKernelGGL((embed_pos_bwd_kernel<float, bf16>), dim3(seq), dim3(256), 0, s, (const float*)dz, (bf16*)grad, batch, seq, h, pos_offset, accumulate);
+  else
+    hipLaunchKernelGGL((embed_pos_bwd_kernel<float, float>), dim3(seq), dim3(256), 0, s, (const float*)dz, (float*)grad, batch, seq, h, pos_offset, accumulate);
+  DTD_LAUNCH_CHECK();
+}
+
+DTD_EXPORT int dtd_dropout(int dtype, const void* x, void* y, size_t n, float p, const uint64_t* rng,
+                           uint32_t stream_id, hipStream_t s) {
+  if (n == 0) return 0;
+  size_t blocks = (n / 8 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  if (dtype == kBF16) hipLaunchKernelGGL(dropout_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, (bf16*)y, n, p, rng, stream_id);
+  else hipLaunchKernelGGL(dropout_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, (float*)y, n, p, rng, stream_id);
+  DTD_LAUNCH_CHECK();
+}

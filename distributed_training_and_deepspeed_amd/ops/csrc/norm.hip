@@ -1,0 +1,364 @@
+// Fused residual-add + dropout + LayerNorm (forward and backward) for gfx950.
+//
+// Replaces the reference's separate ATen kernels for `dropout(y)`, `x + residual` and
+// `nn.LayerNorm` (HF BertSelfOutput/BertOutput post-LN, OPT/GPT-2/BLOOM pre-LN;
+// SURVEY.md K4/K6, reference model/transformer.py:95-104).
+//
+//   forward :  z   = r + dropout(y)            (y or r may be absent)
+//              out = (z - mean) * rstd * gamma + beta
+//   backward:  dz  = rstd * (g - mean(g) - xhat * mean(g * xhat)) + dz_extra,  g = dout * gamma
+//              dy  = dropout_bwd(dz)                              (mask regenerated, not stored)
+//              column partials of dout*xhat (dgamma), dout (dbeta), dy (bias of y's producer)
+//
+// Layout: one 64-lane wave per row while a row fits in registers (h <= 2048), lane l holding
+// VEC contiguous elements at column (c*64 + l)*VEC for c < ITERS, so every access is a
+// coalesced 8/16-byte-per-lane vector access and the two-pass mean/variance stays in registers.
+// Wider rows (the h=9216 estimator block) take a block-per-row kernel.  Column partials
+// are reduced inside the block through LDS and written once per block; `dtd_colsum_finalize`
+// sums them in a fixed order, so parameter gradients are bitwise deterministic (no atomics).
+#include "common.h"
+
+using namespace dtd;
+
+namespace {
+
+struct LnFwdArgs {
+  const void* y; const void* r; const void* gamma; const void* beta;
+  void* z; void* out; float* mean; float* rstd;
+  int rows, h; float eps, p; const uint64_t* rng; uint32_t stream_id;
+};
+
+struct LnBwdArgs {
+  const void* dout; const void* dz_extra; const void* z; const float* mean; const float* rstd;
+  const void* gamma; void* dz; void* dy; float* part_gamma; float* part_beta; float* part_bias;
+  int rows, h; float p; const uint64_t* rng; uint32_t stream_id;
+};
+
+// keep/scale for element e of a [rows, h] tensor.
+__device__ __forceinline__ float drop_factor(const DropoutRng& g, uint64_t e, uint32_t thr, float scale) {
+  uint32_t b = g.bits(e >> 1);
+  uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
+  return h16 >= thr ? scale : 0.f;
+}
+
+template <typename T, int VEC, int ITERS>
+__global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
+  constexpr int NPL = VEC * ITERS;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int h = a.h;
+  const size_t base = (size_t)row * h;
+  const bool has_drop = a.p > 0.f && a.y != nullptr;
+  DropoutRng g(a.rng, a.stream_id);
+  const uint32_t thr = keep_threshold(a.p);
+  const float scale = has_drop ? 1.f / (1.f - a.p) : 1.f;
+  float z[NPL];
+#pragma unroll
+  for (int c = 0; c < ITERS; ++c) {
+    const int col = (c * 64 + lane) * VEC;
+    float t[VEC];
+    if (a.y) {
+      vload<T, VEC>((const T*)a.y + base + col, t);
+      if (has_drop) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) t[j] *= drop_factor(g, base + col + j, thr, scale);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) t[j] = 0.f;
+    }
+    if (a.r) {
+      float rr[VEC];
+      vload<T, VEC>((const T*)a.r + base + col, rr);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) t[j] += rr[j];
+    }
+    if (a.z) vstore<T, VEC>((T*)a.z + base + col, t);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) z[c * VEC + j] = t[j];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) s += z[i];
+  const float mu = wave_sum(s) / h;
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { float d = z[i] - mu; v += d * d; }
+  const float rs = rsqrtf(wave_sum(v) / h + a.eps);
+  if (lane == 0) { a.mean[row] = mu; a.rstd[row] = rs; }
+#pragma unroll
+  for (int c = 0; c < ITERS; ++c) {
+    const int col = (c * 64 + lane) * VEC;
+    float gm[VEC], bt[VEC], o[VEC];
+    vload<T, VEC>((const T*)a.gamma + col, gm);
+    vload<T, VEC>((const T*)a.beta + col, bt);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (z[c * VEC + j] - mu) * rs * gm[j] + bt[j];
+    vstore<T, VEC>((T*)a.out + base + col, o);
+  }
+}
+
+template <typename T, int VEC, int ITERS>
+__global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
+  constexpr int NPL = VEC * ITERS;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int h = a.h;
+  const bool has_drop = a.p > 0.f && a.dy != nullptr;
+  DropoutRng g(a.rng, a.stream_id);
+  const uint32_t thr = keep_threshold(a.p);
+  const float scale = has_drop ? 1.f / (1.f - a.p) : 1.f;
+  float pg[NPL], pb[NPL], py[NPL], gm[NPL];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { pg[i] = 0.f; pb[i] = 0.f; py[i] = 0.f; }
+#pragma unroll
+  for (int c = 0; c < ITERS; ++c) vload<T, VEC>((const T*)a.gamma + (c * 64 + lane) * VEC, gm + c * VEC);
+
+  for (int row = blockIdx.x * nw + w; row < a.rows; row += gridDim.x * nw) {
+    const size_t base = (size_t)row * h;
+    const float mu = a.mean[row], rs = a.rstd[row];
+    float xh[NPL], dg[NPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < ITERS; ++c) {
+      const int col = (c * 64 + lane) * VEC;
+      float zz[VEC], dd[VEC];
+      vload<T, VEC>((const T*)a.z + base + col, zz);
+      vload<T, VEC>((const T*)a.dout + base + col, dd);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const int i = c * VEC + j;
+        xh[i] = (zz[j] - mu) * rs;
+        dg[i] = dd[j] * gm[i];
+        s1 += dg[i];
+        s2 += dg[i] * xh[i];
+        pg[i] += dd[j] * xh[i];
+        pb[i] += dd[j];
+      }
+    }
+    const float m1 = wave_sum(s1) / h, m2 = wave_sum(s2) / h;
+#pragma unroll
+    for (int c = 0; c < ITERS; ++c) {
+      const int col = (c * 64 + lane) * VEC;
+      float dz[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const int i = c * VEC + j;
+        dz[j] = rs * (dg[i] - m1 - xh[i] * m2);
+      }
+      if (a.dz_extra) {
+        float e[VEC];
+        vload<T, VEC>((const T*)a.dz_extra + base + col, e);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) dz[j] += e[j];
+      }
+      if (a.dz) vstore<T, VEC>((T*)a.dz + base + col, dz);
+      if (a.dy) {
+        float dy[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          dy[j] = has_drop ? dz[j] * drop_factor(g, base + col + j, thr, scale) : dz[j];
+          py[c * VEC + j] += dy[j];
+        }
+        vstore<T, VEC>((T*)a.dy + base + col, dy);
+      }
+    }
+  }
+  // Block-level reduction of the column partials through LDS (one array at a time).
+  __shared__ float sh[4][2048];  // nw <= 4 waves, h <= 2048
+  float* outs[3] = {a.part_gamma, a.part_beta, a.part_bias};
+  float* srcs[3] = {pg, pb, py};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (!outs[k]) continue;
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < ITERS; ++c)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) sh[w][(c * 64 + lane) * VEC + j] = srcs[k][c * VEC + j];
+    __syncthreads();
+    for (int col = threadIdx.x; col < h; col += blockDim.x) {
+      float t = 0.f;
+      for (int i = 0; i < nw; ++i) t += sh[i][col];
+      outs[k][(size_t)blockIdx.x * h + col] = t;
+    }
+  }
+}
+
+// ---- generic block-per-row kernels (any even h; used for h > 2048) ----
+template <typename T>
+__global__ void __launch_bounds__(256) ln_fwd_block(LnFwdArgs a) {
+  __shared__ float red[8];
+  const int row = blockIdx.x;
+  const int h = a.h;
+  const size_t base = (size_t)row * h;
+  const bool has_drop = a.p > 0.f && a.y != nullptr;
+  DropoutRng g(a.rng, a.stream_id);
+  const uint32_t thr = keep_threshold(a.p);
+  const float scale = has_drop ? 1.f / (1.f - a.p) : 1.f;
+  float s = 0.f;
+  // pass 1: z, written to a.z or (if absent) recomputed in pass 2/3
+  for (int col = threadIdx.x * 2; col < h; col += blockDim.x * 2) {
+    float t[2] = {0.f, 0.f};
+    if (a.y) {
+      vload<T, 2>((const T*)a.y + base + col, t);
+      if (has_drop) { t[0] *= drop_factor(g, base + col, thr, scale); t[1] *= drop_factor(g, base + col + 1, thr, scale); }
+    }
+    if (a.r) { float rr[2]; vload<T, 2>((const T*)a.r + base + col, rr); t[0] += rr[0]; t[1] += rr[1]; }
+    if (a.z) vstore<T, 2>((T*)a.z + base + col, t);
+    s += t[0] + t[1];
+  }
+  const float mu = block_sum(s, red) / h;
+  auto zval = [&](int col, float* t) {
+    if (a.z) { vload<T, 2>((const T*)a.z + base + col, t); return; }
+    t[0] = t[1] = 0.f;
+    if (a.y) {
+      vload<T, 2>((const T*)a.y + base + col, t);
+      if (has_drop) { t[0] *= drop_factor(g, base + col, thr, scale); t[1] *= drop_factor(g, base + col + 1, thr, scale); }
+    }
+    if (a.r) { float rr[2]; vload<T, 2>((const T*)a.r + base + col, rr); t[0] += rr[0]; t[1] += rr[1]; }
+  };
+  float v = 0.f;
+  for (int col = threadIdx.x * 2; col < h; col += blockDim.x * 2) {
+    float t[2]; zval(col, t);
+    v += (t[0] - mu) * (t[0] - mu) + (t[1] - mu) * (t[1] - mu);
+  }
+  const float rs = rsqrtf(block_sum(v, red) / h + a.eps);
+  if (threadIdx.x == 0) { a.mean[row] = mu; a.rstd[row] = rs; }
+  for (int col = threadIdx.x * 2; col < h; col += blockDim.x * 2) {
+    float t[2], gm[2], bt[2], o[2];
+    zval(col, t);
+    vload<T, 2>((const T*)a.gamma + col, gm);
+    vload<T, 2>((const T*)a.beta + col, bt);
+    o[0] = (t[0] - mu) * rs * gm[0] + bt[0];
+    o[1] = (t[1] - mu) * rs * gm[1] + bt[1];
+    vstore<T, 2>((T*)a.out + base + col, o);
+  }
+}
+
+// Block-per-row backward; column partials accumulate per block over a strided row set in
+// a global partial row (each block owns row blockIdx.x of the partial arrays).
+template <typename T>
+__global__ void __launch_bounds__(256) ln_bwd_block(LnBwdArgs a) {
+  __shared__ float red[8];
+  const int h = a.h;
+  const bool has_drop = a.p > 0.f && a.dy != nullptr;
+  DropoutRng g(a.rng, a.stream_id);
+  const uint32_t thr = keep_threshold(a.p);
+  const float scale = has_drop ? 1.f / (1.f - a.p) : 1.f;
+  float* pgp = a.part_gamma ? a.part_gamma + (size_t)blockIdx.x * h : nullptr;
+  float* pbp = a.part_beta ? a.part_beta + (size_t)blockIdx.x * h : nullptr;
+  float* pyp = a.part_bias ? a.part_bias + (size_t)blockIdx.x * h : nullptr;
+  for (int col = threadIdx.x; col < h; col += blockDim.x) {
+    if (pgp) pgp[col] = 0.f;
+    if (pbp) pbp[col] = 0.f;
+    if (pyp) pyp[col] = 0.f;
+  }
+  __syncthreads();
+  for (int row = blockIdx.x; row < a.rows; row += gridDim.x) {
+    const size_t base = (size_t)row * h;
+    const float mu = a.mean[row], rs = a.rstd[row];
+    float s1 = 0.f, s2 = 0.f;
+    for (int col = threadIdx.x * 2; col < h; col += blockDim.x * 2) {
+      float zz[2], dd[2], gm[2];
+      vload<T, 2>((const T*)a.z + base + col, zz);
+      vload<T, 2>((const T*)a.dout + base + col, dd);
+      vload<T, 2>((const T*)a.gamma + col, gm);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float xh = (zz[j] - mu) * rs, dg = dd[j] * gm[j];
+        s1 += dg; s2 += dg * xh;
+        if (pgp) pgp[col + j] += dd[j] * xh;   // same thread owns the same columns every row
+        if (pbp) pbp[col + j] += dd[j];
+      }
+    }
+    const float m1 = block_sum(s1, red) / h, m2 = block_sum(s2, red) / h;
+    for (int col = threadIdx.x * 2; col < h; col += blockDim.x * 2) {
+      float zz[2], dd[2], gm[2], dz[2];
+      vload<T, 2>((const T*)a.z + base + col, zz);
+      vload<T, 2>((const T*)a.dout + base + col, dd);
+      vload<T, 2>((const T*)a.gamma + col, gm);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float xh = (zz[j] - mu) * rs, dg = dd[j] * gm[j];
+        dz[j] = rs * (dg - m1 - xh * m2);
+      }
+      if (a.dz_extra) { float e[2]; vload<T, 2>((const T*)a.dz_extra + base + col, e); dz[0] += e[0]; dz[1] += e[1]; }
+      if (a.dz) vstore<T, 2>((T*)a.dz + base + col, dz);
+      if (a.dy) {
+        float dy[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          dy[j] = has_drop ? dz[j] * drop_factor(g, base + col + j, thr, scale) : dz[j];
+          if (pyp) pyp[col + j] += dy[j];
+        }
+        vstore<T, 2>((T*)a.dy + base + col, dy);
+      }
+    }
+  }
+}
+
+template <typename T, int VEC, int ITERS>
+bool try_wave(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream_t s) {
+  const int h = f ? f->h : b->h;
+  if (h != 64 * VEC * ITERS) return false;
+  if (f) {
+    const int rows_per_block = 4;
+    hipLaunchKernelGGL((ln_fwd_wave<T, VEC, ITERS>), dim3((f->rows + rows_per_block - 1) / rows_per_block),
+                       dim3(256), 0, s, *f);
+  } else {
+    hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS>), dim3(nblocks_bwd), dim3(256), 0, s, *b);
+  }
+  return true;
+}
+
+template <typename T>
+void dispatch(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream_t s) {
+  if (try_wave<T, 2, 1>(f, b, nblocks_bwd, s)) return;     // h = 128
+  if (try_wave<T, 4, 1>(f, b, nblocks_bwd, s)) return;     // 256
+  if (try_wave<T, 8, 1>(f, b, nblocks_bwd, s)) return;     // 512
+  if (try_wave<T, 4, 3>(f, b, nblocks_bwd, s)) return;     // 768
+  if (try_wave<T, 8, 2>(f, b, nblocks_bwd, s)) return;     // 1024
+  if (try_wave<T, 4, 5>(f, b, nblocks_bwd, s)) return;     // 1280
+  if (try_wave<T, 8, 3>(f, b, nblocks_bwd, s)) return;     // 1536
+  if (try_wave<T, 8, 4>(f, b, nblocks_bwd, s)) return;     // 2048
+  if (f) hipLaunchKernelGGL((ln_fwd_block<T>), dim3(f->rows), dim3(256), 0, s, *f);
+  else hipLaunchKernelGGL((ln_bwd_block<T>), dim3(nblocks_bwd), dim3(256), 0, s, *b);
+}
+
+}  // namespace
+
+// Number of partial rows the backward writes (callers size part_* as [n, h] fp32).
+static bool wave_shape(int h) {
+  return h == 128 || h == 256 || h == 512 || h == 768 || h == 1024 || h == 1280 || h == 1536 || h == 2048;
+}
+DTD_EXPORT int dtd_ln_bwd_num_partials(int rows, int h) {
+  if (wave_shape(h)) {
+    int blocks = (rows + 3) / 4;
+    return blocks < 512 ? blocks : 512;
+  }
+  return rows < 512 ? rows : 512;
+}
+
+DTD_EXPORT int dtd_ln_fwd(int dtype, const void* y, const void* r, const void* gamma, const void* beta,
+                          void* z, void* out, float* mean, float* rstd, int rows, int h, float eps,
+                          float p, const uint64_t* rng, uint32_t stream_id, hipStream_t s) {
+  if (rows <= 0) return 0;
+  LnFwdArgs a{y, r, gamma, beta, z, out, mean, rstd, rows, h, eps, p, rng, stream_id};
+  if (dtype == kBF16) dispatch<bf16>(&a, nullptr, 0, s);
+  else dispatch<float>(&a, nullptr, 0, s);
+  DTD_LAUNCH_CHECK();
+}
+
+DTD_EXPORT int dtd_ln_bwd(int dtype, const void* dout, const void* dz_extra, const void* z,
+                          const float* mean, const float* rstd, const void* gamma, void* dz, void* dy,
+                          float* part_gamma, float* part_beta, float* part_bias, int rows, int h,
+                          float p, const uint64_t* rng, uint32_t stream_id, hipStream_t s) {
+  if (rows <= 0) return 0;
+  LnBwdArgs a{dout, dz_extra, z, mean, rstd, gamma, dz, dy, part_gamma, part_beta, part_bias,
+              rows, h, p, rng, stream_id};
+  const int nb = dtd_ln_bwd_num_partials(rows, h);
+  if (dtype == kBF16) dispatch<bf16>(nullptr, &a, nb, s);
+  else dispatch<float>(nullptr, &a, nb, s);
+  DTD_LAUNCH_CHECK();
+}

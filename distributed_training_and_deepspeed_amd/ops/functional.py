@@ -1,0 +1,353 @@
+"""Functional front-end of the fused ops.
+
+Each function runs the gfx950 HIP kernel for CUDA(HIP) tensors and the PyTorch reference
+(``ops/ref.py`` semantics, same dropout masks) for CPU tensors.  Parameter-gradient outputs
+are written into caller-provided destination tensors (``main_grad`` views of the flat
+gradient buffers, see ``parallel/grad_buffer.py``) with overwrite-or-accumulate semantics,
+which is how the framework avoids a separate gradient-accumulation pass.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .rng import RngState, keep_mask
+
+ACT_CODES = {"none": 0, "gelu": 1, "gelu_tanh": 2, "relu": 3}
+IGNORE_INDEX = -100
+
+
+def _on_gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _c(t):
+    return None if t is None else t.contiguous()
+
+
+# --------------------------------------------------------------------------------------
+# dropout
+# --------------------------------------------------------------------------------------
+def _ref_dropout(x: torch.Tensor, p: float, rng: RngState, sid: int) -> torch.Tensor:
+    if p <= 0.0:
+        return x
+    seed, step = (int(v) for v in rng.state.tolist())
+    keep = keep_mask(x.numel(), p, seed, step, sid, device=x.device).view_as(x)
+    return (x.float() * keep / (1.0 - p)).to(x.dtype)
+
+
+def dropout(x: torch.Tensor, p: float, rng: RngState, sid: int) -> torch.Tensor:
+    if p <= 0.0:
+        return x
+    if not _on_gpu(x):
+        return _ref_dropout(x, p, rng, sid)
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    _lib.call("dtd_dropout", _lib.dt(x), x.data_ptr(), y.data_ptr(), x.numel(), float(p),
+              rng.state.data_ptr(), sid, _lib.stream())
+    return y
+
+
+# --------------------------------------------------------------------------------------
+# residual + dropout + LayerNorm
+# --------------------------------------------------------------------------------------
+def ln_fwd(y, r, gamma, beta, eps: float, p: float, rng: RngState, sid: int, store_z: bool = True):
+    """z = r + dropout(y); out = LN(z).  Returns (z, out, mean, rstd); z is None when it
+    equals an input (no branch) or store_z is False."""
+    ref = y if y is not None else r
+    rows = ref.numel() // ref.shape[-1]
+    h = ref.shape[-1]
+    if not _on_gpu(ref):
+        z = torch.zeros_like(ref, dtype=torch.float32)
+        if y is not None:
+            z = z + _ref_dropout(y, p, rng, sid).float()
+        if r is not None:
+            z = z + r.float()
+        zf = z.view(rows, h)
+        mean = zf.mean(-1)
+        var = zf.var(-1, unbiased=False)
+        rstd = torch.rsqrt(var + eps)
+        out = ((zf - mean[:, None]) * rstd[:, None] * gamma.float() + beta.float()).to(ref.dtype).view_as(ref)
+        zz = z.to(ref.dtype) if (store_z and y is not None) else None
+        return zz, out, mean, rstd
+    y, r = _c(y), _c(r)
+    z = torch.empty_like(ref) if (store_z and y is not None) else None
+    out = torch.empty_like(ref)
+    mean = torch.empty(rows, dtype=torch.float32, device=ref.device)
+    rstd = torch.empty_like(mean)
+    _lib.call("dtd_ln_fwd", _lib.dt(ref), _lib.ptr(y), _lib.ptr(r), gamma.data_ptr(), beta.data_ptr(),
+              _lib.ptr(z), out.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, h, float(eps),
+              float(p if y is not None else 0.0), rng.state.data_ptr(), sid, _lib.stream())
+    return z, out, mean, rstd
+
+
+def _unpack(dst, acc):
+    """Gradient destinations are a tensor (with the call's ``acc``) or a (tensor, acc) pair."""
+    if isinstance(dst, tuple):
+        return dst
+    return dst, acc
+
+
+def _write_grad(dst, val: torch.Tensor, acc: bool) -> None:
+    if dst is None:
+        return
+    dst, acc = _unpack(dst, acc)
+    if acc:
+        dst.add_(val.to(dst.dtype))
+    else:
+        dst.copy_(val)
+
+
+def _finalize(part: torch.Tensor, n: int, cols: int, dst, acc: bool, scale: float = 1.0):
+    if dst is None:
+        return
+    dst, acc = _unpack(dst, acc)
+    _lib.call("dtd_colsum_finalize", part.data_ptr(), n, cols, dst.data_ptr(), _lib.dt(dst), int(acc),
+              float(scale), _lib.stream())
+
+
+def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: int,
+           want_dz: bool = True, want_dy: bool = False,
+           dgamma=None, dbeta=None, dbias=None, acc: bool = False):
+    """Backward of ``ln_fwd``.  Returns (dz, dy); writes dgamma/dbeta/dbias (bias of the
+    producer of y, i.e. column sums of dy) into the destination tensors."""
+    rows = dout.numel() // dout.shape[-1]
+    h = dout.shape[-1]
+    if not _on_gpu(dout):
+        zf = z.float().view(rows, h)
+        xh = (zf - mean[:, None]) * rstd[:, None]
+        d = dout.float().view(rows, h)
+        g = d * gamma.float()
+        m1 = g.mean(-1, keepdim=True)
+        m2 = (g * xh).mean(-1, keepdim=True)
+        dz = rstd[:, None] * (g - m1 - xh * m2)
+        if dz_extra is not None:
+            dz = dz + dz_extra.float().view(rows, h)
+        dy = None
+        if want_dy:
+            dy = _ref_dropout(dz.to(dout.dtype), p, rng, sid) if p > 0 else dz.to(dout.dtype)
+            _write_grad(dbias, dy.float().sum(0), acc)
+            dy = dy.view_as(dout)
+        _write_grad(dgamma, (d * xh).sum(0), acc)
+        _write_grad(dbeta, d.sum(0), acc)
+        return (dz.to(dout.dtype).view_as(dout) if want_dz else None), dy
+    dout, dz_extra = _c(dout), _c(dz_extra)
+    dz = torch.empty_like(dout) if want_dz else None
+    dy = torch.empty_like(dout) if want_dy else None
+    n = _lib.lib().dtd_ln_bwd_num_partials(rows, h)
+    k = int(dgamma is not None) + int(dbeta is not None) + int(dbias is not None and want_dy)
+    part = torch.empty((max(k, 1), n, h), dtype=torch.float32, device=dout.device)
+    slots = iter(range(k))
+    pg = part[next(slots)] if dgamma is not None else None
+    pb = part[next(slots)] if dbeta is not None else None
+    py = part[next(slots)] if (dbias is not None and want_dy) else None
+    _lib.call("dtd_ln_bwd", _lib.dt(dout), dout.data_ptr(), _lib.ptr(dz_extra), z.data_ptr(), mean.data_ptr(),
+              rstd.data_ptr(), gamma.data_ptr(), _lib.ptr(dz), _lib.ptr(dy), _lib.ptr(pg), _lib.ptr(pb),
+              _lib.ptr(py), rows, h, float(p if want_dy else 0.0), rng.state.data_ptr(), sid, _lib.stream())
+    if pg is not None:
+        _finalize(pg, n, h, dgamma, acc)
+    if pb is not None:
+        _finalize(pb, n, h, dbeta, acc)
+    if py is not None:
+        _finalize(py, n, h, dbias, acc)
+    return dz, dy
+
+
+# --------------------------------------------------------------------------------------
+# activations
+# --------------------------------------------------------------------------------------
+def _ref_act(u: torch.Tensor, act: str) -> torch.Tensor:
+    x = u.float()
+    if act == "gelu":
+        y = 0.5 * x * (1.0 + torch.erf(x * 0.7071067811865476))
+    elif act == "gelu_tanh":
+        y = 0.5 * x * (1.0 + torch.tanh(0.7978845608028654 * (x + 0.044715 * x * x * x)))
+    elif act == "relu":
+        y = torch.clamp_min(x, 0.0)
+    else:
+        y = x
+    return y.to(u.dtype)
+
+
+def _ref_act_grad(u: torch.Tensor, act: str) -> torch.Tensor:
+    x = u.float()
+    if act == "gelu":
+        cdf = 0.5 * (1.0 + torch.erf(x * 0.7071067811865476))
+        return cdf + x * 0.3989422804014327 * torch.exp(-0.5 * x * x)
+    if act == "gelu_tanh":
+        k = 0.7978845608028654
+        t = torch.tanh(k * (x + 0.044715 * x ** 3))
+        return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k * (1 + 3 * 0.044715 * x * x)
+    if act == "relu":
+        return (x > 0).float()
+    return torch.ones_like(x)
+
+
+def act_fwd(u: torch.Tensor, act: str) -> torch.Tensor:
+    if act == "none":
+        return u
+    if not _on_gpu(u):
+        return _ref_act(u, act)
+    u = u.contiguous()
+    y = torch.empty_like(u)
+    _lib.call("dtd_act_fwd", _lib.dt(u), u.data_ptr(), y.data_ptr(), u.numel(), ACT_CODES[act], _lib.stream())
+    return y
+
+
+def act_bwd(dy: torch.Tensor, u: torch.Tensor | None, act: str, dbias=None, acc: bool = False,
+            want_du: bool = True):
+    """du = dy * act'(u); writes column sums of du into ``dbias``.  act='none' is a plain
+    bias-gradient column sum of dy (returns dy)."""
+    cols = dy.shape[-1]
+    rows = dy.numel() // cols
+    if not _on_gpu(dy):
+        du = dy.float() if act == "none" else dy.float() * _ref_act_grad(u, act)
+        _write_grad(dbias, du.view(rows, cols).sum(0), acc)
+        return du.to(dy.dtype) if want_du else None
+    dy = dy.contiguous()
+    du = torch.empty_like(dy) if (want_du and act != "none") else None
+    n = _lib.lib().dtd_act_bwd_num_partials(rows, cols)
+    part = torch.empty((n, cols), dtype=torch.float32, device=dy.device) if dbias is not None else None
+    _lib.call("dtd_act_bwd", _lib.dt(dy), dy.data_ptr(), _lib.ptr(u), _lib.ptr(du), _lib.ptr(part), rows, cols,
+              ACT_CODES[act], _lib.stream())
+    if part is not None:
+        _finalize(part, n, cols, dbias, acc)
+    return dy if act == "none" else du
+
+
+def bias_grad(dy: torch.Tensor, dbias: torch.Tensor, acc: bool = False) -> None:
+    act_bwd(dy, None, "none", dbias=dbias, acc=acc, want_du=False)
+
+
+# --------------------------------------------------------------------------------------
+# softmax cross-entropy
+# --------------------------------------------------------------------------------------
+def xent_fwd(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = IGNORE_INDEX):
+    """Returns (mean loss [scalar fp32 tensor], lse [N], stats [2] = (mean, count))."""
+    V = logits.shape[-1]
+    rows = logits.numel() // V
+    labels = labels.reshape(-1)
+    if not _on_gpu(logits):
+        z = logits.float().view(rows, V)
+        lse = torch.logsumexp(z, -1)
+        valid = labels != ignore_index
+        tgt = z.gather(1, labels.clamp_min(0)[:, None])[:, 0]
+        loss_row = torch.where(valid, lse - tgt, torch.zeros_like(lse))
+        cnt = valid.sum().float()
+        mean = loss_row.sum() / cnt
+        return mean, lse, torch.stack([mean, cnt])
+    logits = logits.contiguous()
+    labels = labels.contiguous().to(torch.int64)
+    loss_row = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    lse = torch.empty_like(loss_row)
+    stats = torch.empty(2, dtype=torch.float32, device=logits.device)
+    _lib.call("dtd_xent_fwd", _lib.dt(logits), logits.data_ptr(), labels.data_ptr(), loss_row.data_ptr(),
+              lse.data_ptr(), stats.data_ptr(), rows, V, ignore_index, _lib.stream())
+    return stats[0], lse, stats
+
+
+def xent_bwd(logits, labels, lse, stats, grad_out, ignore_index: int = IGNORE_INDEX):
+    V = logits.shape[-1]
+    rows = logits.numel() // V
+    labels = labels.reshape(-1)
+    if not _on_gpu(logits):
+        z = logits.float().view(rows, V)
+        p = torch.exp(z - lse[:, None])
+        valid = labels != ignore_index
+        p[torch.arange(rows), labels.clamp_min(0)] -= 1.0
+        p = p * valid[:, None].float() * (grad_out.float() / stats[1])
+        return p.to(logits.dtype).view_as(logits)
+    d = torch.empty_like(logits)
+    gout = grad_out.reshape(1).to(torch.float32).contiguous()
+    _lib.call("dtd_xent_bwd", _lib.dt(logits), logits.data_ptr(), labels.contiguous().to(torch.int64).data_ptr(),
+              lse.data_ptr(), stats.data_ptr(), gout.data_ptr(), d.data_ptr(), rows, V, ignore_index,
+              _lib.stream())
+    return d
+
+
+# --------------------------------------------------------------------------------------
+# embeddings
+# --------------------------------------------------------------------------------------
+def embed_fwd(ids: torch.Tensor, word: torch.Tensor, pos: torch.Tensor | None, type_: torch.Tensor | None,
+              seq: int, pos_offset: int = 0, type_ids: torch.Tensor | None = None) -> torch.Tensor:
+    rows = ids.numel()
+    h = word.shape[1]
+    if not _on_gpu(word):
+        flat = ids.reshape(-1)
+        out = word[flat].float()
+        if pos is not None:
+            pidx = torch.arange(rows, device=ids.device) % seq + pos_offset
+            out = out + pos[pidx].float()
+        if type_ is not None:
+            tid = type_ids.reshape(-1) if type_ids is not None else torch.zeros_like(flat)
+            out = out + type_[tid].float()
+        return out.to(word.dtype)
+    out = torch.empty((rows, h), dtype=word.dtype, device=word.device)
+    ids_c = ids.reshape(-1).contiguous().to(torch.int64)
+    tids = type_ids.reshape(-1).contiguous().to(torch.int64) if type_ids is not None else None
+    _lib.call("dtd_embed_fwd", _lib.dt(word), ids_c.data_ptr(), _lib.ptr(tids), word.data_ptr(), _lib.ptr(pos),
+              _lib.ptr(type_), out.data_ptr(), rows, h, seq, pos_offset, _lib.stream())
+    return out
+
+
+def embed_word_bwd(ids: torch.Tensor, dz: torch.Tensor, grad: torch.Tensor, acc: bool, padding_idx: int = -1):
+    flat = ids.reshape(-1)
+    h = grad.shape[1]
+    dz = dz.reshape(-1, h)
+    if not _on_gpu(grad):
+        g = torch.zeros(grad.shape, dtype=torch.float32, device=grad.device)
+        g.index_add_(0, flat, dz.float())
+        if padding_idx >= 0:
+            g[padding_idx] = 0
+        if acc:
+            grad.add_(g.to(grad.dtype))
+        else:
+            grad.copy_(g)
+        return
+    if not acc:
+        grad.zero_()
+    sorted_ids, perm = torch.sort(flat.to(torch.int64), stable=True)
+    dz = dz.contiguous()
+    _lib.call("dtd_embed_word_bwd", _lib.dt(dz), _lib.dt(grad), sorted_ids.data_ptr(), perm.data_ptr(),
+              dz.data_ptr(), grad.data_ptr(), flat.numel(), h, 1, padding_idx, _lib.stream())
+
+
+def embed_pos_bwd(dz: torch.Tensor, grad: torch.Tensor, batch: int, seq: int, pos_offset: int, acc: bool):
+    h = grad.shape[1]
+    if not _on_gpu(grad):
+        s = dz.reshape(batch, seq, h).float().sum(0)
+        if not acc:
+            grad.zero_()
+        grad[pos_offset:pos_offset + seq].add_(s.to(grad.dtype))
+        return
+    if not acc:
+        grad.zero_()
+    dz = dz.contiguous()
+    _lib.call("dtd_embed_pos_bwd", _lib.dt(dz), _lib.dt(grad), dz.data_ptr(), grad.data_ptr(), batch, seq, h,
+              pos_offset, 1, _lib.stream())
+
+
+# --------------------------------------------------------------------------------------
+# flat-buffer utilities
+# --------------------------------------------------------------------------------------
+def scale_cast_(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0, dscale: torch.Tensor | None = None):
+    """dst = src * scale * (dscale[0] if given), with dtype conversion (flat buffers)."""
+    if not _on_gpu(src):
+        v = src.float() * scale
+        if dscale is not None:
+            v = v * dscale[0]
+        dst.copy_(v)
+        return dst
+    _lib.call("dtd_scale_cast", src.data_ptr(), _lib.dt(src), dst.data_ptr(), _lib.dt(dst), src.numel(),
+              float(scale), _lib.ptr(dscale), _lib.stream())
+    return dst
+
+
+def sq_norm(x: torch.Tensor) -> torch.Tensor:
+    """Sum of squares of a flat tensor as a 0-dim fp32 device tensor (no host sync)."""
+    if not _on_gpu(x):
+        return x.float().pow(2).sum()
+    n = _lib.lib().dtd_sqnorm_num_partials(x.numel())
+    part = torch.empty(n, dtype=torch.float32, device=x.device)
+    _lib.call("dtd_sqnorm_partials", x.data_ptr(), _lib.dt(x), x.numel(), part.data_ptr(), _lib.stream())
+    return part.sum()

@@ -1,0 +1,160 @@
+"""Fused Adam/AdamW over flat buffers: one HIP kernel launch per optimizer step.
+
+Replaces DeepSpeed FusedAdam (selected by ``"optimizer": {"type": "Adam"}``,
+zero_dp_training.py:28-33, adam_w_mode=True), ``torch.optim.AdamW``
+(model_parallel_training.py:50) and ``transformers.AdamW`` (data_parallel_training.py:34)
+-- SURVEY.md D12/D21/K9.  Hyper-parameter conventions per script are reproduced by
+``hf_eps`` (transformers: eps added to sqrt(v) before bias correction) and the defaults.
+
+Storage: parameters of the optimizer live in a flat buffer (shared with DDP/ZeRO when the
+model is wrapped, see ``parallel/flat.py``); gradients in the matching flat ``main_grad``
+buffer; fp32 master weights are kept when the model runs in bf16 (the kernel writes the
+updated bf16 copy in the same pass).  Step count, lr and the gradient scale live in a small
+device array so the step is hipGraph-capturable and clipping needs no host sync.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import _lib
+from ..ops import functional as Fx
+from ..parallel.flat import FlatLayout, GradBuffer
+
+MODE_ADAMW, MODE_BIAS_CORR, MODE_HF_EPS = 1, 2, 4
+
+
+def _flat_view_of(t: torch.Tensor, numel: int) -> torch.Tensor:
+    return torch.empty(0, dtype=t.dtype, device=t.device).set_(t.untyped_storage(), 0, (numel,))
+
+
+def adam_reference_(p, m, v, g, lr, b1, b2, eps, wd, step, mode, grad_scale=1.0):
+    """fp32 PyTorch implementation of the kernel math (CPU path and test oracle)."""
+    g = g.float() * grad_scale
+    if not (mode & MODE_ADAMW) and wd != 0:
+        g = g + wd * p
+    m.mul_(b1).add_(g, alpha=1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    if mode & MODE_ADAMW:
+        p.mul_(1 - lr * wd)
+    bc1 = 1 - b1 ** step if mode & MODE_BIAS_CORR else 1.0
+    bc2s = math.sqrt(1 - b2 ** step) if mode & MODE_BIAS_CORR else 1.0
+    if mode & MODE_HF_EPS:
+        p.addcdiv_(m, v.sqrt().add_(eps), value=-lr * bc2s / bc1)
+    else:
+        p.addcdiv_(m, v.sqrt().div_(bc2s).add_(eps), value=-lr / bc1)
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 adam_w_mode: bool = True, bias_correction: bool = True, hf_eps: bool = False,
+                 max_grad_norm: float | None = None):
+        params = list(params)
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
+                        bias_correction=bias_correction)
+        super().__init__(params, defaults)
+        self.mode = (MODE_ADAMW if adam_w_mode else 0) | (MODE_BIAS_CORR if bias_correction else 0) | \
+            (MODE_HF_EPS if hf_eps else 0)
+        self.max_grad_norm = max_grad_norm
+        self._setup()
+
+    # ------------------------------------------------------------------ storage
+    def _setup(self) -> None:
+        ps = [p for g in self.param_groups for p in g["params"] if p.requires_grad]
+        self._params = ps
+        shared = self._detect_shared_flat(ps)
+        if shared is None:
+            layout = FlatLayout(ps)
+            self.param_flat = layout.flatten_params_()
+            self.gbuf = GradBuffer(layout, ps[0].dtype, ps[0].device)
+            self.grad_flat = self.gbuf.buf
+        else:
+            self.param_flat, self.grad_flat = shared
+            self.gbuf = None
+        dev = self.param_flat.device
+        n = self.param_flat.numel()
+        if self.param_flat.dtype == torch.float32:
+            self.master, self.lowp = self.param_flat, None
+        else:
+            self.master, self.lowp = self.param_flat.float(), self.param_flat
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.hp = torch.zeros(8, dtype=torch.float32, device=dev)
+        self._hp_host = None
+        self.step_count = 0
+        self._push_hparams()
+
+    @staticmethod
+    def _detect_shared_flat(ps):
+        """Params already laid out by DDP/ZeRO: one param storage + one main_grad storage."""
+        if not ps or any(getattr(p, "main_grad", None) is None for p in ps):
+            return None
+        st = {p.untyped_storage().data_ptr() for p in ps}
+        gst = {p.main_grad.untyped_storage().data_ptr() for p in ps}
+        if len(st) != 1 or len(gst) != 1:
+            return None
+        if any(p.storage_offset() != p.main_grad.storage_offset() for p in ps):
+            return None
+        numel = ps[0].untyped_storage().nbytes() // ps[0].element_size()
+        gnumel = ps[0].main_grad.untyped_storage().nbytes() // ps[0].main_grad.element_size()
+        if numel != gnumel or sum(p.numel() for p in ps) > numel:
+            return None
+        return _flat_view_of(ps[0], numel), _flat_view_of(ps[0].main_grad, gnumel)
+
+    def _push_hparams(self) -> None:
+        g = self.param_groups[0]
+        host = (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]),
+                float(g["weight_decay"]))
+        if host != self._hp_host:
+            self.hp[:5].copy_(torch.tensor(host, dtype=torch.float32))
+            self.hp[6] = 1.0
+            self._hp_host = host
+
+    # ------------------------------------------------------------------ step
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self._push_hparams()
+        self.step_count += 1
+        self.hp[5:6].add_(1.0)
+        if self.max_grad_norm is not None:
+            norm = Fx.sq_norm(self.grad_flat).sqrt()
+            self.hp[6:7].copy_(torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0).reshape(1))
+        n = self.master.numel()
+        if self.master.is_cuda:
+            _lib.call("dtd_adam_step", self.master.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                      self.grad_flat.data_ptr(), _lib.dt(self.grad_flat), _lib.ptr(self.lowp), n,
+                      self.hp.data_ptr(), self.mode, _lib.stream())
+        else:
+            g = self.param_groups[0]
+            adam_reference_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_flat, g["lr"], g["betas"][0],
+                            g["betas"][1], g["eps"], g["weight_decay"], self.step_count, self.mode,
+                            float(self.hp[6]))
+            if self.lowp is not None:
+                self.lowp.copy_(self.master)
+        if self.gbuf is not None:
+            self.gbuf.reset()
+        return loss
+
+    def zero_grad(self, set_to_none: bool = True):
+        if self.gbuf is not None:
+            self.gbuf.reset()
+        for p in self._params:
+            p.grad = None
+
+    def state_dict(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                "master": self.master, "param_groups": [{k: v for k, v in g.items() if k != "params"}
+                                                         for g in self.param_groups]}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.master.copy_(sd["master"])
+        if self.lowp is not None:
+            self.lowp.copy_(self.master)
+        self.hp[5] = float(self.step_count)
+        for g, s in zip(self.param_groups, sd["param_groups"]):
+            g.update(s)

@@ -1,0 +1,157 @@
+"""Numerics of every gfx950 HIP kernel against the fp32 PyTorch reference of the same op.
+
+The CPU branch of ``ops/functional.py`` is the reference (fp32 math on the same inputs,
+bit-identical dropout masks), so each test runs the op once on the GPU (kernel) and once on
+CPU copies of the inputs.
+"""
+import pytest
+import torch
+
+from distributed_training_and_deepspeed_amd.ops import _lib
+from distributed_training_and_deepspeed_amd.ops import functional as Fx
+from distributed_training_and_deepspeed_amd.ops.rng import RngState, keep_mask
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rng_pair(seed=7, step=3):
+    g = RngState(seed, device=DEV)
+    c = RngState(seed, device="cpu")
+    g.state[1] = step
+    c.state[1] = step
+    return g, c
+
+
+def close(a, b, tol):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale} (tol {tol})"
+
+
+def test_library_loads_and_is_native():
+    lib = _lib.lib()
+    assert lib is not None and hasattr(lib, "dtd_ln_fwd")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_dropout_mask_matches_reference(dtype):
+    g, c = rng_pair()
+    x = torch.ones(1000003, dtype=dtype, device=DEV)
+    y = Fx.dropout(x, 0.1, g, 77)
+    keep = keep_mask(x.numel(), 0.1, 7, 3, 77)
+    assert torch.equal((y.cpu() != 0), keep)
+    frac = keep.float().mean().item()
+    assert abs(frac - 0.9) < 0.002
+
+
+@pytest.mark.parametrize("h", [128, 768, 1024, 384, 2304])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_layernorm_fwd_bwd(h, dtype):
+    torch.manual_seed(0)
+    rows = 300
+    g, c = rng_pair()
+    y = torch.randn(rows, h, dtype=dtype)
+    r = torch.randn(rows, h, dtype=dtype)
+    gamma = (1 + 0.1 * torch.randn(h)).to(dtype)
+    beta = (0.1 * torch.randn(h)).to(dtype)
+    dout = torch.randn(rows, h, dtype=dtype)
+    dext = torch.randn(rows, h, dtype=dtype)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    outs = {}
+    for dev, rng in ((DEV, g), ("cpu", c)):
+        z, o, m, rs = Fx.ln_fwd(y.to(dev), r.to(dev), gamma.to(dev), beta.to(dev), 1e-5, 0.1, rng, 5)
+        dg = torch.zeros(h, dtype=torch.float32, device=dev)
+        db = torch.zeros(h, dtype=torch.float32, device=dev)
+        dbias = torch.zeros(h, dtype=torch.float32, device=dev)
+        dz, dy = Fx.ln_bwd(dout.to(dev), dext.to(dev), z, m, rs, gamma.to(dev), 0.1, rng, 5, want_dz=True,
+                           want_dy=True, dgamma=dg, dbeta=db, dbias=dbias)
+        outs[dev] = (z, o, m, rs, dz, dy, dg, db, dbias)
+    for a, b in zip(outs[DEV], outs["cpu"]):
+        close(a, b, tol)
+
+
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "relu"])
+def test_activation_fwd_bwd(act):
+    torch.manual_seed(1)
+    u = torch.randn(257, 3072, dtype=torch.bfloat16)
+    dy = torch.randn_like(u)
+    res = {}
+    for dev in (DEV, "cpu"):
+        a = Fx.act_fwd(u.to(dev), act)
+        db = torch.zeros(3072, dtype=torch.float32, device=dev)
+        du = Fx.act_bwd(dy.to(dev), u.to(dev), act, dbias=db)
+        res[dev] = (a, du, db)
+    for a, b in zip(res[DEV], res["cpu"]):
+        close(a, b, 2e-2)
+
+
+@pytest.mark.parametrize("V", [28996, 50257, 1000, 250880])
+def test_softmax_xent(V):
+    torch.manual_seed(2)
+    rows = 64
+    z = (3 * torch.randn(rows, V)).to(torch.bfloat16)
+    lab = torch.randint(0, V, (rows,))
+    lab[::3] = -100
+    gout = torch.tensor(0.7)
+    res = {}
+    for dev in (DEV, "cpu"):
+        loss, lse, st = Fx.xent_fwd(z.to(dev), lab.to(dev))
+        d = Fx.xent_bwd(z.to(dev), lab.to(dev), lse, st, gout.to(dev))
+        res[dev] = (loss, lse, st, d)
+    ref = torch.nn.functional.cross_entropy(z.float(), lab, ignore_index=-100)
+    close(res[DEV][0], ref, 1e-4)
+    for a, b in zip(res[DEV], res["cpu"]):
+        close(a, b, 2e-2)
+
+
+def test_embedding_fwd_bwd():
+    torch.manual_seed(3)
+    V, h, B, S = 1000, 768, 4, 64
+    word = torch.randn(V, h, dtype=torch.bfloat16)
+    pos = torch.randn(S + 2, h, dtype=torch.bfloat16)
+    typ = torch.randn(2, h, dtype=torch.bfloat16)
+    ids = torch.randint(0, 50, (B, S))  # many repeats -> exercises segment sums
+    dz = torch.randn(B * S, h, dtype=torch.bfloat16)
+    res = {}
+    for dev in (DEV, "cpu"):
+        out = Fx.embed_fwd(ids.to(dev), word.to(dev), pos.to(dev), typ.to(dev), S, 2)
+        gw = torch.full((V, h), 0.5, dtype=torch.float32, device=dev)
+        gp = torch.zeros(S + 2, h, dtype=torch.float32, device=dev)
+        Fx.embed_word_bwd(ids.to(dev), dz.to(dev), gw, True, padding_idx=0)
+        Fx.embed_pos_bwd(dz.to(dev), gp, B, S, 2, False)
+        res[dev] = (out, gw, gp)
+    for a, b in zip(res[DEV], res["cpu"]):
+        close(a, b, 2e-2)
+
+
+@pytest.mark.parametrize("hf", [False, True])
+def test_fused_adam_matches_reference(hf):
+    from distributed_training_and_deepspeed_amd.optim.fused_adam import (MODE_ADAMW, MODE_BIAS_CORR, MODE_HF_EPS,
+                                                                          adam_reference_)
+    torch.manual_seed(4)
+    n = 100003
+    p = torch.randn(n)
+    m = torch.randn(n).abs() * 0.1
+    v = torch.randn(n).abs() * 0.01
+    gr = torch.randn(n).to(torch.bfloat16)
+    mode = MODE_ADAMW | MODE_BIAS_CORR | (MODE_HF_EPS if hf else 0)
+    hp = torch.tensor([1e-3, 0.9, 0.999, 1e-6, 0.01, 3.0, 0.5, 0.0], device=DEV)
+    pg, mg, vg = p.to(DEV), m.to(DEV), v.to(DEV)
+    lowp = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    _lib.call("dtd_adam_step", pg.data_ptr(), mg.data_ptr(), vg.data_ptr(), gr.to(DEV).data_ptr(), 1, lowp.data_ptr(),
+              n, hp.data_ptr(), mode, _lib.stream())
+    adam_reference_(p, m, v, gr, 1e-3, 0.9, 0.999, 1e-6, 0.01, 3, mode, grad_scale=0.5)
+    close(pg, p, 1e-5)
+    close(mg, m, 1e-5)
+    close(vg, v, 1e-5)
+    close(lowp, p, 1e-2)
+
+
+def test_sqnorm_and_scale_cast():
+    x = torch.randn(123457, device=DEV).to(torch.bfloat16)
+    close(Fx.sq_norm(x), x.float().pow(2).sum(), 1e-4)
+    y = torch.empty(x.numel(), dtype=torch.float32, device=DEV)
+    Fx.scale_cast_(x, y, 0.25)
+    close(y, x.float() * 0.25, 1e-6)
