@@ -68,6 +68,8 @@ def main():
     cfg = get_config(args.model)
     model = build_model(args.model, impl=args.impl, dtype=dtype, device=device, seed=1234,
                         sparse_mlm_head=not args.dense_mlm_head)
+    if args.impl == "reference":
+        model.rt.exact_dropout = False  # torch-eager baseline: ATen dropout, HF-style eager ops
     model.train()
     gdt = {"bf16": torch.bfloat16, "fp32": torch.float32}.get(args.grad_dtype, dtype)
     ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt)

@@ -60,31 +60,48 @@ __global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ u, T
 }
 
 // du = dy * act'(u) (act == kNone: du = dy), column partials of du per row-group.
-// grid = (col_tiles, row_groups); block = 128 threads x 8 columns = 1024-column tile.
-template <typename T>
+// grid = (col_tiles, row_groups); block = 128 threads x VEC columns.
+template <typename T, int VEC>
 __global__ void __launch_bounds__(128) act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ u,
                                                       T* __restrict__ du, float* __restrict__ part,
                                                       int rows, int cols, int act) {
-  const int col = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  const int col = (blockIdx.x * blockDim.x + threadIdx.x) * VEC;
   if (col >= cols) return;
-  float acc[8];
+  float acc[VEC];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
   for (int r = blockIdx.y; r < rows; r += gridDim.y) {
     const size_t off = (size_t)r * cols + col;
-    float d[8];
-    vload<T, 8>(dy + off, d);
+    float d[VEC];
+    vload<T, VEC>(dy + off, d);
     if (act != kNone) {
-      float x[8];
-      vload<T, 8>(u + off, x);
+      float x[VEC];
+      vload<T, VEC>(u + off, x);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] *= act_df(act, x[j]);
+      for (int j = 0; j < VEC; ++j) d[j] *= act_df(act, x[j]);
     }
-    if (du) vstore<T, 8>(du + off, d);
+    if (du) vstore<T, VEC>(du + off, d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += d[j];
+    for (int j = 0; j < VEC; ++j) acc[j] += d[j];
   }
-  if (part) vstore<float, 8>(part + (size_t)blockIdx.y * cols + col, acc);
+  if (part) vstore<float, VEC>(part + (size_t)blockIdx.y * cols + col, acc);
+}
+
+template <typename T, int VEC>
+void launch_act_bwd(const void* dy, const void* u, void* du, float* part, int rows, int cols, int act, int groups,
+                    hipStream_t s) {
+  dim3 grid((cols / VEC + 127) / 128, groups);
+  hipLaunchKernelGGL((act_bwd_kernel<T, VEC>), grid, dim3(128), 0, s, (const T*)dy, (const T*)u, (T*)du, part, rows,
+                     cols, act);
+}
+
+template <typename T>
+void dispatch_act_bwd(const void* dy, const void* u, void* du, float* part, int rows, int cols, int act, int groups,
+                      hipStream_t s) {
+  if (cols % 8 == 0) launch_act_bwd<T, 8>(dy, u, du, part, rows, cols, act, groups, s);
+  else if (cols % 4 == 0) launch_act_bwd<T, 4>(dy, u, du, part, rows, cols, act, groups, s);
+  else if (cols % 2 == 0) launch_act_bwd<T, 2>(dy, u, du, part, rows, cols, act, groups, s);
+  else launch_act_bwd<T, 1>(dy, u, du, part, rows, cols, act, groups, s);
 }
 
 // out[c] = (accumulate ? out[c] : 0) + sum_p part[p][c]; fixed summation order.
@@ -133,12 +150,9 @@ DTD_EXPORT int dtd_act_bwd_num_partials(int rows, int cols) {
 DTD_EXPORT int dtd_act_bwd(int dtype, const void* dy, const void* u, void* du, float* part, int rows, int cols,
                            int act, hipStream_t s) {
   if (rows <= 0) return 0;
-  if (cols % 8) return (int)hipErrorInvalidValue;
-  dim3 grid((cols + 1023) / 1024, dtd_act_bwd_num_partials(rows, cols));
-  if (dtype == kBF16)
-    hipLaunchKernelGGL(act_bwd_kernel<bf16>, grid, dim3(128), 0, s, (const bf16*)dy, (const bf16*)u, (bf16*)du, part, rows, cols, act);
-  else
-    hipLaunchKernelGGL(act_bwd_kernel<float>, grid, dim3(128), 0, s, (const float*)dy, (const float*)u, (float*)du, part, rows, cols, act);
+  const int groups = dtd_act_bwd_num_partials(rows, cols);
+  if (dtype == kBF16) dispatch_act_bwd<bf16>(dy, u, du, part, rows, cols, act, groups, s);
+  else dispatch_act_bwd<float>(dy, u, du, part, rows, cols, act, groups, s);
   DTD_LAUNCH_CHECK();
 }
 

@@ -102,8 +102,10 @@ def test_softmax_xent(V):
         res[dev] = (loss, lse, st, d)
     ref = torch.nn.functional.cross_entropy(z.float(), lab, ignore_index=-100)
     close(res[DEV][0], ref, 1e-4)
-    for a, b in zip(res[DEV], res["cpu"]):
-        close(a, b, 2e-2)
+    valid = lab != -100  # the kernel writes lse = 0 for ignored rows
+    close(res[DEV][1][valid.to(DEV)], res["cpu"][1][valid], 1e-4)
+    close(res[DEV][2], res["cpu"][2], 1e-4)
+    close(res[DEV][3], res["cpu"][3], 2e-2)
 
 
 def test_embedding_fwd_bwd():
