@@ -134,13 +134,12 @@ def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, 
     dctx = dctx.contiguous()
     dqkv = torch.empty_like(qkv)
     delta = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
-    dq_acc = torch.zeros((B, H, S, D), dtype=torch.float32, device=qkv.device)
     sl = slopes.to(device=qkv.device, dtype=torch.float32).contiguous() if slopes is not None else None
     ld = 3 * H * D
     es = qkv.element_size()
     qb, gb = qkv.data_ptr(), dqkv.data_ptr()
     _lib.call("dtd_attn_bwd", qb, qb + H * D * es, qb + 2 * H * D * es, ctx.data_ptr(), dctx.data_ptr(),
-              lse.data_ptr(), delta.data_ptr(), dq_acc.data_ptr(), gb, gb + H * D * es, gb + 2 * H * D * es,
+              lse.data_ptr(), delta.data_ptr(), None, gb, gb + H * D * es, gb + 2 * H * D * es,
               _lib.ptr(sl), B, S, H, D, ld, H * D, int(causal), 0, 0, 1.0 / math.sqrt(D), float(p),
               rng.state.data_ptr() if rng is not None else None, sid, _lib.stream())
     return dqkv

@@ -70,6 +70,7 @@ __global__ void __launch_bounds__(128) act_bwd_kernel(const T* __restrict__ dy, 
   float acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+#pragma unroll 4
   for (int r = blockIdx.y; r < rows; r += gridDim.y) {
     const size_t off = (size_t)r * cols + col;
     float d[VEC];
@@ -104,25 +105,44 @@ void dispatch_act_bwd(const void* dy, const void* u, void* du, float* part, int 
   else launch_act_bwd<T, 1>(dy, u, du, part, rows, cols, act, groups, s);
 }
 
-// out[c] = (accumulate ? out[c] : 0) + sum_p part[p][c]; fixed summation order.
-// block = 256 threads = 64 columns x 4 part-slices, combined through LDS.
-template <typename O>
-__global__ void __launch_bounds__(256) colsum_finalize_kernel(const float* __restrict__ part, int nparts, int cols,
-                                                              O* __restrict__ out, int accumulate, float scale) {
-  __shared__ float sh[4][64];
+// out[c] = (accumulate ? out[c] : 0) + scale * sum_p part[p][c]; fixed summation order.
+// block = 1024 threads = 64 columns x 16 part-slices combined through LDS; grid.y selects one
+// of up to 4 (part, out) pairs so the LayerNorm backward finalises gamma/beta/bias in one launch.
+struct FinalizeSet {
+  const float* part[4]; void* out[4]; int dtype[4]; int acc[4];
+};
+
+__global__ void __launch_bounds__(1024) colsum_finalize_kernel(FinalizeSet fs, int nparts, int cols, float scale) {
+  __shared__ float sh[16][65];
   const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
-  float t = 0.f;
+  const int k = blockIdx.y;
+  const float* part = fs.part[k];
+  float t0 = 0.f, t1 = 0.f;
   if (col < cols) {
-    for (int p = sl; p < nparts; p += 4) t += part[(size_t)p * cols + col];
+    int p = sl;
+    for (; p + 16 < nparts; p += 32) {
+      t0 += part[(size_t)p * cols + col];
+      t1 += part[(size_t)(p + 16) * cols + col];
+    }
+    if (p < nparts) t0 += part[(size_t)p * cols + col];
   }
-  sh[sl][lane] = t;
+  sh[sl][lane] = t0 + t1;
   __syncthreads();
   if (sl == 0 && col < cols) {
-    float s = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += sh[i][lane];
     s *= scale;
-    if (accumulate) s += (float)out[col];
-    out[col] = (O)s;
+    if (fs.dtype[k] == kBF16) {
+      bf16* o = (bf16*)fs.out[k];
+      if (fs.acc[k]) s += (float)o[col];
+      o[col] = (bf16)s;
+    } else {
+      float* o = (float*)fs.out[k];
+      if (fs.acc[k]) s += o[col];
+      o[col] = s;
+    }
   }
 }
 
@@ -141,7 +161,7 @@ DTD_EXPORT int dtd_act_fwd(int dtype, const void* u, void* y, size_t n, int act,
 // Row groups used by dtd_act_bwd for a [rows, cols] operand (callers size `part` [n, cols]).
 DTD_EXPORT int dtd_act_bwd_num_partials(int rows, int cols) {
   const int tiles = (cols + 1023) / 1024;
-  int g = 1024 / tiles;
+  int g = 512 / tiles;
   if (g < 1) g = 1;
   if (g > rows) g = rows;
   return g;
@@ -159,10 +179,23 @@ DTD_EXPORT int dtd_act_bwd(int dtype, const void* dy, const void* u, void* du, f
 DTD_EXPORT int dtd_colsum_finalize(const float* part, int nparts, int cols, void* out, int out_dtype, int accumulate,
                                    float scale, hipStream_t s) {
   if (cols <= 0) return 0;
-  dim3 grid((cols + 63) / 64);
-  if (out_dtype == kBF16)
-    hipLaunchKernelGGL(colsum_finalize_kernel<bf16>, grid, dim3(256), 0, s, part, nparts, cols, (bf16*)out, accumulate, scale);
-  else
-    hipLaunchKernelGGL(colsum_finalize_kernel<float>, grid, dim3(256), 0, s, part, nparts, cols, (float*)out, accumulate, scale);
+  FinalizeSet fs{};
+  fs.part[0] = part; fs.out[0] = out; fs.dtype[0] = out_dtype; fs.acc[0] = accumulate;
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 63) / 64, 1), dim3(1024), 0, s, fs, nparts, cols, scale);
+  DTD_LAUNCH_CHECK();
+}
+
+// Up to 4 partial arrays laid out back to back in `parts` ([n][nparts][cols]).
+DTD_EXPORT int dtd_colsum_finalize_multi(int n, const float* parts, int nparts, int cols, void* out0, int dt0, int acc0,
+                                         void* out1, int dt1, int acc1, void* out2, int dt2, int acc2, hipStream_t s) {
+  if (cols <= 0 || n <= 0) return 0;
+  FinalizeSet fs{};
+  void* outs[3] = {out0, out1, out2};
+  int dts[3] = {dt0, dt1, dt2}, accs[3] = {acc0, acc1, acc2};
+  for (int i = 0; i < n && i < 3; ++i) {
+    fs.part[i] = parts + (size_t)i * nparts * cols;
+    fs.out[i] = outs[i]; fs.dtype[i] = dts[i]; fs.acc[i] = accs[i];
+  }
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 63) / 64, n), dim3(1024), 0, s, fs, nparts, cols, 1.f);
   DTD_LAUNCH_CHECK();
 }

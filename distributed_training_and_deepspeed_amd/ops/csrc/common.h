@@ -171,11 +171,11 @@ struct DropoutRng {
     k0 = mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + 0x9e3779b9U));
     k1 = mix32((uint32_t)step * 0x85ebca6bU ^ mix32(stream_id + 0x632be5abU) ^ k0);
   }
-  // 32 random bits for 64-bit element index i.
+  // 32 random bits for 64-bit element index i (one mix32 per pair of dropout decisions:
+  // the attention kernels draw B*H*S*S of them per layer, so the hash is kept short).
   __device__ __forceinline__ uint32_t bits(uint64_t i) const {
-    uint32_t lo = (uint32_t)i, hi = (uint32_t)(i >> 32);
-    uint32_t h = mix32(lo * 0x9e3779b1U + k0);
-    return mix32(h ^ (hi * 0xc2b2ae35U) ^ k1);
+    const uint32_t lo = (uint32_t)i, hi = (uint32_t)(i >> 32);
+    return mix32(((lo * 0x9e3779b1U) ^ k0) + ((hi * 0xc2b2ae35U) ^ k1));
   }
 };
 // Two keep-decisions per 32 random bits (16-bit thresholds: p quantised to 1/65536).

@@ -69,6 +69,61 @@ __global__ void __launch_bounds__(256) embed_word_bwd_kernel(const int64_t* __re
   }
 }
 
+// Chunked variant for skewed id distributions (e.g. thousands of [MASK] tokens in one MLM
+// batch): pass 1 sums runs of at most CH rows of one id into fp32 scratch rows (one workgroup
+// per chunk), pass 2 adds a segment's chunk sums in order into the table row.  seg_lo/seg_hi
+// are the [first, last+1) sorted positions of each position's id (searchsorted left/right).
+constexpr int kChunk = 16;
+
+template <typename T>
+__global__ void __launch_bounds__(256) embed_chunk_sum_kernel(const int64_t* __restrict__ perm,
+                                                              const int64_t* __restrict__ seg_lo,
+                                                              const int64_t* __restrict__ seg_hi,
+                                                              const T* __restrict__ dz, float* __restrict__ scratch,
+                                                              int h) {
+  const int i = blockIdx.x;
+  const int lo = (int)seg_lo[i];
+  if ((i - lo) % kChunk) return;
+  const int end = min(i + kChunk, (int)seg_hi[i]);
+  for (int c = threadIdx.x * 2; c < h; c += blockDim.x * 2) {
+    float acc[2] = {0.f, 0.f};
+    for (int k = i; k < end; ++k) {
+      float x[2];
+      vload<T, 2>(dz + (size_t)perm[k] * h + c, x);
+      acc[0] += x[0]; acc[1] += x[1];
+    }
+    vstore<float, 2>(scratch + (size_t)i * h + c, acc);
+  }
+}
+
+template <typename G>
+__global__ void __launch_bounds__(256) embed_chunk_add_kernel(const int64_t* __restrict__ sorted_ids,
+                                                              const int64_t* __restrict__ seg_lo,
+                                                              const int64_t* __restrict__ seg_hi,
+                                                              const float* __restrict__ scratch, G* __restrict__ grad,
+                                                              int h, int accumulate, int padding_idx) {
+  const int i = blockIdx.x;
+  if (seg_lo[i] != i) return;
+  const int64_t id = sorted_ids[i];
+  if (id == padding_idx) return;
+  const int hi = (int)seg_hi[i];
+  G* g = grad + (size_t)id * h;
+  for (int c = threadIdx.x * 2; c < h; c += blockDim.x * 2) {
+    float acc[2] = {0.f, 0.f};
+    for (int k = i; k < hi; k += kChunk) {
+      float x[2];
+      vload<float, 2>(scratch + (size_t)k * h + c, x);
+      acc[0] += x[0]; acc[1] += x[1];
+    }
+    if (accumulate) {
+      float old[2];
+      vload<G, 2>(g + c, old);
+      acc[0] += old[0]; acc[1] += old[1];
+    }
+    vstore<G, 2>(g + c, acc);
+  }
+}
+
 // grad_pos[s + offset] (+)= sum_b dz[b*seq + s]; grid = seq rows.
 template <typename T, typename G>
 __global__ void __launch_bounds__(256) embed_pos_bwd_kernel(const T* __restrict__ dz, G* __restrict__ grad, int batch,
@@ -167,5 +222,20 @@ DTD_EXPORT int dtd_dropout(int dtype, const void* x, void* y, size_t n, float p,
   if (blocks > 4096) blocks = 4096;
   if (dtype == kBF16) hipLaunchKernelGGL(dropout_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, (bf16*)y, n, p, rng, stream_id);
   else hipLaunchKernelGGL(dropout_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, (float*)y, n, p, rng, stream_id);
+  DTD_LAUNCH_CHECK();
+}
+
+DTD_EXPORT int dtd_embed_word_bwd_chunked(int dtype, int grad_dtype, const int64_t* sorted_ids, const int64_t* perm,
+                                          const int64_t* seg_lo, const int64_t* seg_hi, float* scratch, const void* dz,
+                                          void* grad, int rows, int h, int accumulate, int padding_idx, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(embed_chunk_sum_kernel<bf16>, dim3(rows), dim3(256), 0, s, perm, seg_lo, seg_hi, (const bf16*)dz, scratch, h);
+  else
+    hipLaunchKernelGGL(embed_chunk_sum_kernel<float>, dim3(rows), dim3(256), 0, s, perm, seg_lo, seg_hi, (const float*)dz, scratch, h);
+  if (grad_dtype == kBF16)
+    hipLaunchKernelGGL(embed_chunk_add_kernel<bf16>, dim3(rows), dim3(256), 0, s, sorted_ids, seg_lo, seg_hi, scratch, (bf16*)grad, h, accumulate, padding_idx);
+  else
+    hipLaunchKernelGGL(embed_chunk_add_kernel<float>, dim3(rows), dim3(256), 0, s, sorted_ids, seg_lo, seg_hi, scratch, (float*)grad, h, accumulate, padding_idx);
   DTD_LAUNCH_CHECK();
 }

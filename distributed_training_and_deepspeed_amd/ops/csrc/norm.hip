@@ -335,9 +335,9 @@ static bool wave_shape(int h) {
 DTD_EXPORT int dtd_ln_bwd_num_partials(int rows, int h) {
   if (wave_shape(h)) {
     int blocks = (rows + 3) / 4;
-    return blocks < 512 ? blocks : 512;
+    return blocks < 256 ? blocks : 256;
   }
-  return rows < 512 ? rows : 512;
+  return rows < 256 ? rows : 256;
 }
 
 DTD_EXPORT int dtd_ln_fwd(int dtype, const void* y, const void* r, const void* gamma, const void* beta,

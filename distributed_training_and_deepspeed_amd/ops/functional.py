@@ -144,12 +144,16 @@ def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: i
     _lib.call("dtd_ln_bwd", _lib.dt(dout), dout.data_ptr(), _lib.ptr(dz_extra), z.data_ptr(), mean.data_ptr(),
               rstd.data_ptr(), gamma.data_ptr(), _lib.ptr(dz), _lib.ptr(dy), _lib.ptr(pg), _lib.ptr(pb),
               _lib.ptr(py), rows, h, float(p if want_dy else 0.0), rng.state.data_ptr(), sid, _lib.stream())
-    if pg is not None:
-        _finalize(pg, n, h, dgamma, acc)
-    if pb is not None:
-        _finalize(pb, n, h, dbeta, acc)
-    if py is not None:
-        _finalize(py, n, h, dbias, acc)
+    dsts = [d for d, on in ((dgamma, pg is not None), (dbeta, pb is not None), (dbias, py is not None)) if on]
+    if dsts:
+        args = []
+        for d in dsts + [None] * (3 - len(dsts)):
+            if d is None:
+                args += [None, 0, 0]
+            else:
+                t, a = _unpack(d, acc)
+                args += [t.data_ptr(), _lib.dt(t), int(a)]
+        _lib.call("dtd_colsum_finalize_multi", len(dsts), part.data_ptr(), n, h, *args, _lib.stream())
     return dz, dy
 
 
@@ -307,9 +311,13 @@ def embed_word_bwd(ids: torch.Tensor, dz: torch.Tensor, grad: torch.Tensor, acc:
     if not acc:
         grad.zero_()
     sorted_ids, perm = torch.sort(flat.to(torch.int64), stable=True)
+    lo = torch.searchsorted(sorted_ids, sorted_ids, right=False)
+    hi = torch.searchsorted(sorted_ids, sorted_ids, right=True)
     dz = dz.contiguous()
-    _lib.call("dtd_embed_word_bwd", _lib.dt(dz), _lib.dt(grad), sorted_ids.data_ptr(), perm.data_ptr(),
-              dz.data_ptr(), grad.data_ptr(), flat.numel(), h, 1, padding_idx, _lib.stream())
+    scratch = torch.empty((flat.numel(), h), dtype=torch.float32, device=dz.device)
+    _lib.call("dtd_embed_word_bwd_chunked", _lib.dt(dz), _lib.dt(grad), sorted_ids.data_ptr(), perm.data_ptr(),
+              lo.data_ptr(), hi.data_ptr(), scratch.data_ptr(), dz.data_ptr(), grad.data_ptr(), flat.numel(), h, 1,
+              padding_idx, _lib.stream())
 
 
 def embed_pos_bwd(dz: torch.Tensor, grad: torch.Tensor, batch: int, seq: int, pos_offset: int, acc: bool):
