@@ -59,40 +59,73 @@ __global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ u, T
   }
 }
 
-// du = dy * act'(u) (act == kNone: du = dy), column partials of du per row-group.
-// grid = (col_tiles, row_groups); block = 128 threads x VEC columns.
+// du = dy * act'(u) (act == kNone: du = dy), plus per-block column partials of du.
+// grid = (ceil(cols / (64*VEC)), G); block = 4 waves sharing one 64*VEC-column tile; each wave
+// strides over rows with 4 rows in flight (ILP), and the 4 waves' column sums are combined
+// through LDS into one partial row per block row-group.
 template <typename T, int VEC>
-__global__ void __launch_bounds__(128) act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ u,
+__global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ u,
                                                       T* __restrict__ du, float* __restrict__ part,
                                                       int rows, int cols, int act) {
-  const int col = (blockIdx.x * blockDim.x + threadIdx.x) * VEC;
-  if (col >= cols) return;
+  __shared__ float sh[4][64 * VEC];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = (blockIdx.x * 64 + lane) * VEC;
+  const bool cv = col < cols;
   float acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
-#pragma unroll 4
-  for (int r = blockIdx.y; r < rows; r += gridDim.y) {
-    const size_t off = (size_t)r * cols + col;
-    float d[VEC];
-    vload<T, VEC>(dy + off, d);
-    if (act != kNone) {
-      float x[VEC];
-      vload<T, VEC>(u + off, x);
+  const int stride = gridDim.y * 4;
+  int r = blockIdx.y * 4 + w;
+  if (cv) {
+    for (; r + 3 * stride < rows; r += 4 * stride) {
+      float d[4][VEC], x[4][VEC];
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) d[j] *= act_df(act, x[j]);
+      for (int k = 0; k < 4; ++k) {
+        const size_t off = (size_t)(r + k * stride) * cols + col;
+        vload<T, VEC>(dy + off, d[k]);
+        if (act != kNone) vload<T, VEC>(u + off, x[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (act != kNone) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) d[k][j] *= act_df(act, x[k][j]);
+        }
+        if (du) vstore<T, VEC>(du + (size_t)(r + k * stride) * cols + col, d[k]);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] += d[k][j];
+      }
     }
-    if (du) vstore<T, VEC>(du + off, d);
+    for (; r < rows; r += stride) {
+      const size_t off = (size_t)r * cols + col;
+      float d[VEC];
+      vload<T, VEC>(dy + off, d);
+      if (act != kNone) {
+        float x[VEC];
+        vload<T, VEC>(u + off, x);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] += d[j];
+        for (int j = 0; j < VEC; ++j) d[j] *= act_df(act, x[j]);
+      }
+      if (du) vstore<T, VEC>(du + off, d);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += d[j];
+    }
   }
-  if (part) vstore<float, VEC>(part + (size_t)blockIdx.y * cols + col, acc);
+  if (!part) return;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) sh[w][lane * VEC + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 64 * VEC; c += 256) {
+    const int gc = blockIdx.x * 64 * VEC + c;
+    if (gc < cols) part[(size_t)blockIdx.y * cols + gc] = (sh[0][c] + sh[1][c]) + (sh[2][c] + sh[3][c]);
+  }
 }
 
 template <typename T, int VEC>
 void launch_act_bwd(const void* dy, const void* u, void* du, float* part, int rows, int cols, int act, int groups,
                     hipStream_t s) {
-  dim3 grid((cols / VEC + 127) / 128, groups);
-  hipLaunchKernelGGL((act_bwd_kernel<T, VEC>), grid, dim3(128), 0, s, (const T*)dy, (const T*)u, (T*)du, part, rows,
+  dim3 grid((cols / VEC + 63) / 64, groups);
+  hipLaunchKernelGGL((act_bwd_kernel<T, VEC>), grid, dim3(256), 0, s, (const T*)dy, (const T*)u, (T*)du, part, rows,
                      cols, act);
 }
 
@@ -160,10 +193,10 @@ DTD_EXPORT int dtd_act_fwd(int dtype, const void* u, void* y, size_t n, int act,
 
 // Row groups used by dtd_act_bwd for a [rows, cols] operand (callers size `part` [n, cols]).
 DTD_EXPORT int dtd_act_bwd_num_partials(int rows, int cols) {
-  const int tiles = (cols + 1023) / 1024;
-  int g = 512 / tiles;
+  (void)cols;
+  int g = (rows + 15) / 16;
   if (g < 1) g = 1;
-  if (g > rows) g = rows;
+  if (g > 256) g = 256;
   return g;
 }
 
