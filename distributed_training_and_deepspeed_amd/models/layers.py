@@ -20,7 +20,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..ops import functional as Fx
-from ..ops.grad import emit_gemm_grad, grad_done, grad_dst, note_use
+from ..ops.grad import emit_wgrad, grad_done, grad_dst, note_use
 
 from .config import TransformerConfig
 from .transformer import Runtime, init_linear_, ref_dropout
@@ -193,7 +193,7 @@ class _MLMHeadFn(torch.autograd.Function):
         del logits
         Fx.bias_grad(dlogits, *grad_dst(head.decoder_bias))
         grad_done(head.decoder_bias)
-        emit_gemm_grad(head.decoder_weight, dlogits.t(), t)
+        emit_wgrad(head.decoder_weight, dlogits, t)
         dt = dlogits @ head.decoder_weight
         da, _ = Fx.ln_bwd(dt, None, a, m, r, head.ln_g, 0.0, head.rt.rng, 0, want_dz=True,
                           dgamma=grad_dst(head.ln_g), dbeta=grad_dst(head.ln_b))
@@ -201,7 +201,7 @@ class _MLMHeadFn(torch.autograd.Function):
         grad_done(head.ln_b)
         du = Fx.act_bwd(da, u, c.activation, dbias=grad_dst(head.dense_b))
         grad_done(head.dense_b)
-        emit_gemm_grad(head.dense_w, du.t(), x)
+        emit_wgrad(head.dense_w, du, x)
         dx = du @ head.dense_w
         return (dx, None, None) + (None,) * len(head.params())
 
@@ -271,7 +271,7 @@ class _LMHeadFn(torch.autograd.Function):
         x, labels, logits, lse, stats = ctx.saved_tensors
         w = ctx.head.weight
         dlogits = Fx.xent_bwd(logits, labels, lse, stats, gloss)
-        emit_gemm_grad(w, dlogits.t(), x)
+        emit_wgrad(w, dlogits, x)
         return dlogits @ w, None, None, None
 
 

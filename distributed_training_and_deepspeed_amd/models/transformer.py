@@ -25,7 +25,7 @@ from torch import nn
 
 from ..ops import attention as A
 from ..ops import functional as Fx
-from ..ops.grad import emit_gemm_grad, grad_done, grad_dst, note_use
+from ..ops.grad import emit_wgrad, grad_done, grad_dst, note_use
 from ..ops.rng import RngState
 from .config import TransformerConfig
 
@@ -218,11 +218,11 @@ class _FusedLayerFn(torch.autograd.Function):
             for p in (g2, b2, bf2):
                 grad_done(p)
         a = Fx.act_fwd(u, c.activation)
-        emit_gemm_grad(w2, dy.t(), a)
+        emit_wgrad(w2, dy, a)
         da = dy @ w2
         du = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1))
         grad_done(bf1)
-        emit_gemm_grad(w1, du.t(), f_in)
+        emit_wgrad(w1, du, f_in)
         if c.pre_ln:
             dfin = du @ w1
             # z1 = x + dropout(o); f_in = LN2(z1); dz1 also receives dout (residual of out)
@@ -237,20 +237,20 @@ class _FusedLayerFn(torch.autograd.Function):
                                 dgamma=_acc(g1), dbeta=_acc(b1), dbias=_acc(o_b))
             for p in (g1, b1, o_b):
                 grad_done(p)
-        emit_gemm_grad(o_w, do.t(), actx)
+        emit_wgrad(o_w, do, actx)
         dctx = do @ o_w
         dqkv = A.attn_bwd(dctx, qkv, actx, lse, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa)
         Fx.bias_grad(dqkv, *_pair(qkv_b))
         grad_done(qkv_b)
         if c.pre_ln:
-            emit_gemm_grad(qkv_w, dqkv.t(), a_in)
+            emit_wgrad(qkv_w, dqkv, a_in)
             dain = dqkv @ qkv_w
             dx, _ = Fx.ln_bwd(dain, dz1, x2d, m1, r1, g1, 0.0, rng, 0, want_dz=True, want_dy=False,
                               dgamma=_acc(g1), dbeta=_acc(b1))
             for p in (g1, b1):
                 grad_done(p)
         else:
-            emit_gemm_grad(qkv_w, dqkv.t(), x2d)
+            emit_wgrad(qkv_w, dqkv, x2d)
             dx = torch.addmm(dz1, dqkv, qkv_w)
         return (dx.view(B, S, h), None) + (None,) * 12
 
