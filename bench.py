@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--impl", default="fused", choices=["fused", "reference"])
     ap.add_argument("--dense-mlm-head", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
     return ap.parse_args()
 
 
@@ -59,8 +60,12 @@ def main():
     from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
 
     cuda = torch.cuda.is_available()
+    tuned = False
     if cuda:
         torch.cuda.set_device(local)
+        if not args.no_tuned_gemms and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
+            from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
+            tuned = use_tuned_gemms()
     device = torch.device("cuda", local) if cuda else torch.device("cpu")
     if world > 1:
         comm.init(rank=rank, world_size=world, local_rank=local)
@@ -98,7 +103,7 @@ def main():
     for i in range(args.warmup):
         loss = step(i)
     sync()
-    first_loss = float(loss) if args.warmup else float("nan")
+    first_loss = float(loss.detach()) if args.warmup else float("nan")
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -137,9 +142,10 @@ def main():
                 "impl": args.impl,
                 "mlm_head": "dense" if args.dense_mlm_head else "sparse (labelled rows only; identical loss/grads)",
                 "optimizer": "fused AdamW (transformers.AdamW hyper-params, lr 5e-5)",
+                "tuned_gemms": tuned,
             },
             "loss_first": round(first_loss, 4),
-            "loss_last": round(float(loss), 4),
+            "loss_last": round(float(loss.detach()), 4),
         }
         print(json.dumps(res), flush=True)
     if world > 1:

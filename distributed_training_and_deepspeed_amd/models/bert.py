@@ -40,6 +40,14 @@ class BertForMaskedLM(nn.Module):
     def from_config(cls, name: str, **kw) -> "BertForMaskedLM":
         return cls(get_config(name), **kw)
 
+    def zero3_units(self):
+        """Parameter-gathering units for ZeRO-3, in forward order."""
+        return [self.embeddings, *self.layers, self.head]
+
+    def zero3_persistent(self):
+        """Parameters shared between units (tied decoder / word embeddings)."""
+        return [self.embeddings.word] if self.head.decoder_w is None else []
+
     def encode(self, input_ids: torch.Tensor) -> torch.Tensor:
         x = self.embeddings(input_ids)
         for layer in self.layers:
@@ -51,7 +59,7 @@ class BertForMaskedLM(nn.Module):
         x = self.encode(input_ids)
         out = MaskedLMOutput()
         if labels is not None:
-            out.loss = self.head.loss(x, labels)
+            out.loss = self.head(x, labels)
         if labels is None or return_logits:
             out.logits = self.head.logits(x)
         return out

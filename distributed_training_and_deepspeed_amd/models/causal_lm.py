@@ -42,6 +42,14 @@ class CausalLM(nn.Module):
     def from_config(cls, name: str, **kw) -> "CausalLM":
         return cls(get_config(name), **kw)
 
+    def zero3_units(self):
+        """Parameter-gathering units for ZeRO-3, in forward order."""
+        return [self.embeddings, *self.layers] + ([self.final_ln] if self.final_ln is not None else [])
+
+    def zero3_persistent(self):
+        """Parameters shared between units (LM head tied to the word embeddings)."""
+        return [self.embeddings.word]
+
     def encode(self, input_ids: torch.Tensor) -> torch.Tensor:
         x = self.embeddings(input_ids)
         for layer in self.layers:
@@ -55,7 +63,7 @@ class CausalLM(nn.Module):
         x = self.encode(input_ids)
         out = CausalLMOutput()
         if labels is not None:
-            out.loss = self.head.loss(x, labels)
+            out.loss = self.head(x, labels)
         if labels is None or return_logits:
             out.logits = self.head.logits(x)
         return out

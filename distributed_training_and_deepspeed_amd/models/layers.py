@@ -233,6 +233,10 @@ class MLMHead(nn.Module):
     def params(self):
         return (self.dense_w, self.dense_b, self.ln_g, self.ln_b, self.decoder_weight, self.decoder_bias)
 
+    def forward(self, x: torch.Tensor, labels: torch.Tensor | None = None) -> torch.Tensor:
+        """Loss when labels are given, else logits (module call so ZeRO-3 unit hooks fire)."""
+        return self.loss(x, labels) if labels is not None else self.logits(x)
+
     def logits(self, x: torch.Tensor) -> torch.Tensor:
         """Full [.., V] prediction scores (differentiable through autograd)."""
         c = self.cfg
@@ -284,6 +288,9 @@ class LMHead(nn.Module):
     @property
     def weight(self):
         return self._tied[0]
+
+    def forward(self, x: torch.Tensor, labels: torch.Tensor | None = None) -> torch.Tensor:
+        return self.loss(x, labels) if labels is not None else self.logits(x)
 
     def logits(self, x):
         return F.linear(x, self.weight)

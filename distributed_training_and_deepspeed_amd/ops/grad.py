@@ -22,6 +22,9 @@ import torch
 
 def grad_dst(p: torch.Tensor):
     """(destination tensor, accumulate?) for the next gradient contribution of ``p``."""
+    pre = getattr(p, "_dtd_pre_write_hook", None)
+    if pre is not None:  # ZeRO-2/3: materialise the landing bucket on first write
+        pre(p)
     mg = getattr(p, "main_grad", None)
     if mg is not None:
         return mg, bool(getattr(p, "_dtd_touched", False))

@@ -59,6 +59,30 @@ class FusedAdam(torch.optim.Optimizer):
         self.max_grad_norm = max_grad_norm
         self._setup()
 
+    @classmethod
+    def from_flat(cls, master: torch.Tensor, grad: torch.Tensor, lowp: torch.Tensor | None = None, **kw):
+        """Optimizer over pre-built flat buffers (a ZeRO partition): fp32 ``master`` weights,
+        matching ``grad`` buffer and optional low-precision copy written by the kernel.
+        ``param_groups[0]['params'] == [master]`` so its numel is the local partition size."""
+        self = cls.__new__(cls)
+        defaults = dict(lr=kw.pop("lr", 1e-3), betas=tuple(kw.pop("betas", (0.9, 0.999))), eps=kw.pop("eps", 1e-8),
+                        weight_decay=kw.pop("weight_decay", 0.0), bias_correction=kw.get("bias_correction", True))
+        torch.optim.Optimizer.__init__(self, [master], defaults)
+        self.mode = (MODE_ADAMW if kw.get("adam_w_mode", True) else 0) | \
+            (MODE_BIAS_CORR if kw.get("bias_correction", True) else 0) | (MODE_HF_EPS if kw.get("hf_eps", False) else 0)
+        self.max_grad_norm = kw.get("max_grad_norm")
+        self._params = []
+        self.param_flat, self.grad_flat, self.gbuf = master, grad, None
+        self.master, self.lowp = master, lowp
+        dev, n = master.device, master.numel()
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.hp = torch.zeros(8, dtype=torch.float32, device=dev)
+        self._hp_host = None
+        self.step_count = 0
+        self._push_hparams()
+        return self
+
     # ------------------------------------------------------------------ storage
     def _setup(self) -> None:
         ps = [p for g in self.param_groups for p in g["params"] if p.requires_grad]
@@ -119,7 +143,11 @@ class FusedAdam(torch.optim.Optimizer):
         self.step_count += 1
         self.hp[5:6].add_(1.0)
         if self.max_grad_norm is not None:
-            norm = Fx.sq_norm(self.grad_flat).sqrt()
+            sq = Fx.sq_norm(self.grad_flat)
+            red = getattr(self, "_reduce_sqnorm", None)  # ZeRO: sum over partitions (C11)
+            if red is not None:
+                sq = red(sq)
+            norm = sq.sqrt()
             self.hp[6:7].copy_(torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0).reshape(1))
         n = self.master.numel()
         if self.master.is_cuda:

@@ -1,0 +1,583 @@
+"""ZeRO data parallelism, stages 0-3, with a DeepSpeed-style engine API.
+
+Reference: ``deepspeed.initialize(model, model_parameters, config)`` -> (engine, optimizer, _, _),
+``engine(input_ids, labels=...)``, ``engine.backward(loss)``, ``engine.step()``,
+``engine.zero_optimization_stage()`` and ``optimizer.param_groups[0]`` printing the *local*
+partition size (zero_dp_training.py:26-57,81-94).
+
+MI355X-first design (flat buffers, RCCL collectives on contiguous slices, no flatten copies):
+
+* Parameters are grouped into *segments*.  A segment is a contiguous range of a flat buffer
+  whose length is a multiple of world*64; rank r owns chunk r of EVERY segment, so gradient
+  reduction is one ``reduce_scatter_tensor`` per segment and the parameter refresh one
+  ``all_gather_into_tensor`` per segment -- no per-parameter "reduce to owner" calls.
+  Each rank's chunks are packed into one shard buffer (fp32 master, Adam moments, gradient
+  shard, low-precision copy), so the optimizer step is ONE fused-Adam launch per rank.
+* stage 0: segments = ``allreduce_bucket_size`` buckets, gradients all-reduced (replicated
+  optimizer state, DeepSpeed's "stage 0").
+* stage 1: optimizer states partitioned; full gradient buffer, reduce-scatter after backward.
+* stage 2: + gradients partitioned: a bucket's gradient landing buffer is allocated from the
+  caching allocator on its first write, reduce-scattered on the comm stream as soon as the
+  bucket is complete (overlapping the rest of backward) and released -- only the local
+  gradient shard persists.
+* stage 3: + parameters partitioned: every model unit (embeddings, each transformer layer,
+  head) keeps only its parameter shard; the unit is all-gathered on the comm stream before
+  its forward/backward (with one-unit-ahead prefetch) and released after, and its gradients
+  are reduce-scattered as soon as its backward finishes.  Parameters shared between units
+  (tied word embeddings) stay replicated with stage-2 treatment.
+* Collectives go through ``comm.logger`` (the DeepSpeed comms-logger equivalent).
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from .. import comm
+from ..comm import logger as clog
+from ..optim.fused_adam import FusedAdam
+from .flat import ALIGN, unique_params
+
+DEFAULTS = {
+    "train_micro_batch_size_per_gpu": 1,
+    "gradient_accumulation_steps": 1,
+    "gradient_clipping": 0.0,
+    "optimizer": {"type": "Adam", "params": {"lr": 1e-3}},
+    "comms_logger": {"enabled": False},
+    "zero_optimization": {"stage": 0, "reduce_bucket_size": 5e8, "allgather_bucket_size": 5e8,
+                          "overlap_comm": None, "stage3_prefetch_bucket_size": 5e7},
+}
+
+
+class ZeroConfig:
+    def __init__(self, cfg: dict | None):
+        cfg = dict(cfg or {})
+        self.raw = cfg
+        self.micro_batch = int(cfg.get("train_micro_batch_size_per_gpu", 1))
+        self.gas = int(cfg.get("gradient_accumulation_steps", 1))
+        self.clip = float(cfg.get("gradient_clipping", 0.0) or 0.0)
+        opt = dict(DEFAULTS["optimizer"])
+        opt.update(cfg.get("optimizer", {}))
+        self.opt_type = str(opt.get("type", "Adam"))
+        self.opt_params = dict(opt.get("params", {}))
+        self.comms_logger = dict(cfg.get("comms_logger", {}))
+        z = dict(DEFAULTS["zero_optimization"])
+        z.update(cfg.get("zero_optimization", {}))
+        self.stage = int(z.get("stage", 0))
+        if self.stage not in (0, 1, 2, 3):
+            raise ValueError(f"ZeRO stage must be 0-3, got {self.stage}")
+        self.reduce_bucket = int(float(z.get("reduce_bucket_size", 5e8)))
+        self.allreduce_bucket = int(float(cfg.get("allreduce_bucket_size", z.get("allreduce_bucket_size", 5e8))))
+        self.allgather_bucket = int(float(z.get("allgather_bucket_size", 5e8)))
+        oc = z.get("overlap_comm")
+        self.overlap = (self.stage >= 2) if oc is None else bool(oc)
+        bf = cfg.get("bf16", {})
+        self.bf16 = bool(bf.get("enabled", False)) if isinstance(bf, dict) else bool(bf)
+
+
+class _Segment:
+    __slots__ = ("index", "params", "shapes", "offsets", "numel", "chunk", "shard_off", "full", "gbuf", "ready",
+                 "launched", "unit", "gather_event", "module", "pending_release")
+
+    def __init__(self, index, params, world):
+        self.index = index
+        self.params = params
+        self.shapes = [tuple(p.shape) for p in params]  # kept: stage-3 params are emptied between uses
+        self.offsets, off = [], 0
+        for p in params:
+            self.offsets.append(off)
+            off += -(-p.numel() // ALIGN) * ALIGN
+        q = world * ALIGN
+        self.numel = max(q, -(-off // q) * q)
+        self.chunk = self.numel // world
+        self.shard_off = 0
+        self.full = None      # full param buffer (persistent: view into flat; unit: gathered tensor)
+        self.gbuf = None      # full gradient landing buffer
+        self.ready = 0
+        self.launched = False
+        self.unit = False
+        self.gather_event = None
+        self.module = None
+        self.pending_release = False
+
+    def view(self, flat: torch.Tensor, i: int) -> torch.Tensor:
+        shape = self.shapes[i]
+        n = math.prod(shape)
+        return flat[self.offsets[i]:self.offsets[i] + n].view(shape)
+
+
+def _split_buckets(params, cap_elems: int):
+    buckets, cur, size = [], [], 0
+    for p in params:
+        n = -(-p.numel() // ALIGN) * ALIGN
+        if cur and size + n > cap_elems:
+            buckets.append(cur)
+            cur, size = [], 0
+        cur.append(p)
+        size += n
+    if cur:
+        buckets.append(cur)
+    return buckets
+
+
+class ZeroEngine(nn.Module):
+    def __init__(self, model: nn.Module, config: dict | None = None, model_parameters=None, process_group=None):
+        super().__init__()
+        self.module = model
+        self.config = ZeroConfig(config)
+        if not dist.is_initialized():
+            comm.init()
+        self.group = process_group
+        self.world = dist.get_world_size(process_group)
+        self.rank = dist.get_rank(process_group)
+        self.backend = dist.get_backend(process_group)
+        clog.comms_logger.configure(self.config.comms_logger)
+        self.stage = self.config.stage
+        params = unique_params(model_parameters if model_parameters is not None else model.parameters())
+        p0 = params[0]
+        self.device, self.dtype = p0.device, p0.dtype
+        self.grad_dtype = p0.dtype
+        self.cuda = self.device.type == "cuda"
+        self.comm_stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self.shard_world = 1 if self.stage == 0 else self.world
+        self.shard_rank = 0 if self.stage == 0 else self.rank
+        self.micro_step = 0
+        self.global_steps = 0
+        self._callback_queued = False
+        self._need_reset = True
+
+        # ---- partition parameters into persistent buckets and (stage 3) units
+        units, persistent = [], params
+        if self.stage == 3:
+            units, persistent = self._plan_units(model, params)
+        cap = self.config.reduce_bucket if self.stage > 0 else self.config.allreduce_bucket
+        order = list(reversed(persistent))  # ~ gradient-ready order
+        self.buckets = [_Segment(i, b, self.shard_world) for i, b in enumerate(_split_buckets(order, max(cap, ALIGN)))]
+        self.units = []
+        for i, (mod, ps) in enumerate(units):
+            s = _Segment(len(self.buckets) + i, ps, self.world)
+            s.unit, s.module = True, mod
+            self.units.append(s)
+        self.segments = self.buckets + self.units
+        off = 0
+        for s in self.segments:
+            s.shard_off = off
+            off += s.chunk
+        self.shard_numel = off
+        self._seg_of = {}
+        for s in self.segments:
+            for i, p in enumerate(s.params):
+                self._seg_of[id(p)] = (s, i)
+
+        self._broadcast_initial(params)
+        self._build_storage()
+        self._install_grad_hooks()
+        if self.stage == 3:
+            self._install_unit_hooks()
+        self.optimizer = self._build_optimizer()
+
+    # ================================================================== planning
+    def _plan_units(self, model, params):
+        mods = model.zero3_units() if hasattr(model, "zero3_units") else list(model.children())
+        shared = {id(p) for p in (model.zero3_persistent() if hasattr(model, "zero3_persistent") else [])}
+        owner, units = {}, []
+        for m in mods:
+            ps = [p for p in unique_params(m.parameters()) if id(p) not in shared]
+            for p in ps:
+                owner.setdefault(id(p), []).append(m)
+        multi = {k for k, v in owner.items() if len(v) > 1}
+        shared |= multi
+        placed = set()
+        for m in mods:
+            ps = [p for p in unique_params(m.parameters()) if id(p) not in shared and id(p) not in placed]
+            placed.update(id(p) for p in ps)
+            if ps:
+                units.append((m, ps))
+        persistent = [p for p in params if id(p) not in placed]
+        return units, persistent
+
+    @torch.no_grad()
+    def _broadcast_initial(self, params) -> None:
+        if self.world > 1:
+            for p in params:  # C6: every rank starts from rank 0's weights
+                clog.broadcast(p.data, src=0, group=self.group)
+
+    # ================================================================== storage
+    @torch.no_grad()
+    def _build_storage(self) -> None:
+        dev, dt = self.device, self.dtype
+        P = self.shard_numel
+        self.master = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.lowp = torch.zeros(P, dtype=dt, device=dev) if dt != torch.float32 else None
+        self.gshard = torch.zeros(P, dtype=self.grad_dtype, device=dev)
+        self._gtmp = None
+        # persistent buckets: one flat replicated param buffer
+        total = sum(s.numel for s in self.buckets)
+        self.param_flat = torch.zeros(total, dtype=dt, device=dev)
+        off = 0
+        for s in self.buckets:
+            s.full = self.param_flat[off:off + s.numel]
+            for i, p in enumerate(s.params):
+                v = s.view(s.full, i)
+                v.copy_(p.data)
+                p.data = v
+            off += s.numel
+        self.grad_flat = None
+        if self.stage <= 1:
+            self.grad_flat = torch.zeros(total, dtype=self.grad_dtype, device=dev)
+            off = 0
+            for s in self.buckets:
+                s.gbuf = self.grad_flat[off:off + s.numel]
+                for i, p in enumerate(s.params):
+                    p.main_grad = s.view(s.gbuf, i)
+                off += s.numel
+        # master shard: chunk `shard_rank` of every segment
+        for s in self.buckets:
+            lo = self.shard_rank * s.chunk
+            self.master[s.shard_off:s.shard_off + s.chunk].copy_(s.full[lo:lo + s.chunk])
+            if self.lowp is not None:
+                self.lowp[s.shard_off:s.shard_off + s.chunk].copy_(s.full[lo:lo + s.chunk])
+        for s in self.units:
+            full = torch.zeros(s.numel, dtype=dt, device=dev)
+            for i, p in enumerate(s.params):
+                s.view(full, i).copy_(p.data)
+            lo = self.rank * s.chunk
+            self.master[s.shard_off:s.shard_off + s.chunk].copy_(full[lo:lo + s.chunk])
+            if self.lowp is not None:
+                self.lowp[s.shard_off:s.shard_off + s.chunk].copy_(full[lo:lo + s.chunk])
+            self._set_released(s)
+        if self.stage == 0:
+            # replicated optimizer: the shard IS the whole flat buffer -- alias instead of copying
+            self.gshard = self.grad_flat
+            if self.lowp is not None:
+                self.lowp = self.param_flat
+            else:
+                self.master = self.param_flat
+        if self.lowp is None:  # fp32 model: the master shard is the parameter shard
+            self.lowp_view = self.master
+        else:
+            self.lowp_view = self.lowp
+
+    def _set_released(self, s: _Segment) -> None:
+        for p in s.params:
+            p.data = torch.empty(0, dtype=self.dtype, device=self.device)
+        s.full = None
+
+    def _build_optimizer(self) -> FusedAdam:
+        op = dict(self.config.opt_params)
+        t = self.config.opt_type.lower()
+        kw = dict(lr=float(op.get("lr", 1e-3)), betas=tuple(op.get("betas", (0.9, 0.999))),
+                  eps=float(op.get("eps", 1e-8)), weight_decay=float(op.get("weight_decay", 0.0)),
+                  adam_w_mode=(t in ("adamw",) or bool(op.get("adam_w_mode", True))),
+                  bias_correction=bool(op.get("bias_correction", True)))
+        if self.config.clip > 0:
+            kw["max_grad_norm"] = self.config.clip
+        opt = FusedAdam.from_flat(self.master, self.gshard, self.lowp, **kw)
+        if self.stage > 0 and self.world > 1:
+            def _red(sq):
+                clog.all_reduce(sq, op=dist.ReduceOp.SUM, group=self.group)
+                return sq
+            opt._reduce_sqnorm = _red
+        return opt
+
+    # ================================================================== gradient flow
+    def _install_grad_hooks(self) -> None:
+        self._hooks = []
+        for s in self.segments:
+            for p in s.params:
+                p._dtd_ready_hook = self._on_ready
+                p._dtd_touched = False
+                p._dtd_pending = 0
+                if self.stage >= 2 or s.unit:
+                    p._dtd_pre_write_hook = self._pre_write
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._from_autograd))
+
+    def _from_autograd(self, p) -> None:
+        g = p.grad
+        if g is None:
+            return
+        dst_pre = getattr(p, "_dtd_pre_write_hook", None)
+        if dst_pre is not None:
+            dst_pre(p)
+        if p._dtd_touched:
+            p.main_grad.add_(g.to(p.main_grad.dtype))
+        else:
+            p.main_grad.copy_(g)
+        p.grad = None
+        p._dtd_touched = True
+        self._on_ready(p, autograd=True)
+
+    def _pre_write(self, p) -> None:
+        s, _ = self._seg_of[id(p)]
+        if s.gbuf is None:
+            self._alloc_landing(s)
+
+    def _alloc_landing(self, s: _Segment) -> None:
+        s.gbuf = torch.zeros(s.numel, dtype=self.grad_dtype, device=self.device)
+        for i, p in enumerate(s.params):
+            p.main_grad = s.view(s.gbuf, i)
+            p._dtd_touched = False
+
+    def _on_ready(self, p, autograd: bool = False) -> None:
+        if not self._callback_queued and torch.is_grad_enabled() is False:
+            pass
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+        pend = getattr(p, "_dtd_pending", 0)
+        if pend > 0 and not autograd:
+            pend -= 1
+            p._dtd_pending = pend
+            if pend > 0:
+                return
+        s, _ = self._seg_of[id(p)]
+        s.ready += 1
+        if self.stage <= 1 and not self.is_gradient_accumulation_boundary():
+            return
+        if s.ready == len(s.params) and self.config.overlap:
+            if s.unit:
+                self._reduce_unit(s)
+            else:
+                self._launch_ready_buckets_in_order()
+
+    def _launch_ready_buckets_in_order(self) -> None:
+        for s in self.buckets:
+            if s.launched:
+                continue
+            if s.ready < len(s.params):
+                return
+            self._reduce_segment(s)
+
+    def _comm_ctx(self):
+        if self.comm_stream is None:
+            return contextlib.nullcontext()
+        self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
+        return torch.cuda.stream(self.comm_stream)
+
+    def _reduce_segment(self, s: _Segment) -> None:
+        """Reduce one segment's gradients: all-reduce (stage 0) or reduce-scatter into the
+        local gradient shard (stages 1-3); stage 2/3 landing buffers are released after."""
+        s.launched = True
+        for p in s.params:  # parameters without a gradient this step contribute zeros
+            if not p._dtd_touched and s.gbuf is not None:
+                p.main_grad.zero_()
+        if s.gbuf is None:
+            self._alloc_landing(s)
+        buf = s.gbuf
+        # stages 0/1 accumulate micro-batches in the full gradient buffer and reduce once;
+        # stages 2/3 reduce every micro-batch and accumulate the shards
+        first = self.micro_step == 0 or self.stage <= 1
+        out = self.gshard[s.shard_off:s.shard_off + s.chunk]
+        with self._comm_ctx():
+            if self.stage == 0:  # buf aliases the gradient "shard" (the full buffer)
+                if self.world > 1:
+                    op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
+                    w = clog.all_reduce(buf, op=op, group=self.group, async_op=True)
+                    w.wait()
+                    if self.backend != "nccl":
+                        buf.div_(self.world)
+            else:
+                dst = out if first else self._tmp()[s.shard_off:s.shard_off + s.chunk]
+                if self.world > 1:
+                    op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
+                    w = clog.reduce_scatter_tensor(dst, buf, op=op, group=self.group, async_op=True)
+                    w.wait()
+                    if self.backend != "nccl":
+                        dst.div_(self.world)
+                else:
+                    dst.copy_(buf)
+                if not first:
+                    out.add_(dst)
+        if self.stage >= 2 or s.unit:
+            if self.comm_stream is not None:
+                buf.record_stream(self.comm_stream)
+            s.gbuf = None
+            for p in s.params:
+                p.main_grad = None
+
+    def _tmp(self) -> torch.Tensor:
+        if self._gtmp is None:
+            self._gtmp = torch.zeros_like(self.gshard)
+        return self._gtmp
+
+    def _end_of_backward(self) -> None:
+        self._callback_queued = False
+        if self.stage <= 1 and not self.is_gradient_accumulation_boundary():
+            return
+        for s in self.buckets:
+            if not s.launched:
+                self._reduce_segment(s)
+        for s in self.units:
+            if not s.launched:
+                self._reduce_unit(s)
+        if self.comm_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+
+    # ================================================================== stage 3 units
+    def _install_unit_hooks(self) -> None:
+        for k, s in enumerate(self.units):
+            s.module.register_forward_pre_hook(self._make_pre_fwd(k))
+            s.module.register_forward_hook(self._make_post_fwd(k))
+
+    def _gather(self, s: _Segment) -> None:
+        if s.full is not None:
+            return
+        full = torch.empty(s.numel, dtype=self.dtype, device=self.device)
+        src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
+        with self._comm_ctx():
+            if self.world > 1:
+                w = clog.all_gather_into_tensor(full, src, group=self.group, async_op=True)
+                w.wait()
+            else:
+                full.copy_(src)
+            if self.comm_stream is not None:
+                ev = torch.cuda.Event()
+                ev.record(self.comm_stream)
+                s.gather_event = ev
+        s.full = full
+        for i, p in enumerate(s.params):
+            p.data = s.view(full, i)
+
+    def _ensure(self, s: _Segment) -> None:
+        self._gather(s)
+        if s.gather_event is not None:
+            torch.cuda.current_stream(self.device).wait_event(s.gather_event)
+            s.gather_event = None
+
+    def _release(self, s: _Segment) -> None:
+        if s.full is None:
+            return
+        if self.cuda:
+            s.full.record_stream(torch.cuda.current_stream(self.device))
+        self._set_released(s)
+
+    def _make_pre_fwd(self, k: int):
+        def hook(mod, args):
+            if self._need_reset:
+                self._reset()
+            self._ensure(self.units[k])
+            if k + 1 < len(self.units):
+                self._gather(self.units[k + 1])  # prefetch the next unit
+        return hook
+
+    def _make_post_fwd(self, k: int):
+        def hook(mod, args, out):
+            s = self.units[k]
+            if torch.is_grad_enabled() and self.module.training:
+                t = out if torch.is_tensor(out) else None
+                if t is not None and t.requires_grad:
+                    t.register_hook(self._make_bwd_start(k))
+            self._release(s)
+        return hook
+
+    def _make_bwd_start(self, k: int):
+        def hook(grad):
+            s = self.units[k]
+            self._ensure(s)
+            if s.gbuf is None:
+                self._alloc_landing(s)
+            if k > 0:
+                self._gather(self.units[k - 1])  # prefetch the previous unit for its backward
+            return grad
+        return hook
+
+    def _reduce_unit(self, s: _Segment) -> None:
+        if s.launched:
+            return
+        self._reduce_segment(s)
+        self._release(s)
+
+    # ================================================================== engine API
+    def _reset(self) -> None:
+        accumulate_full = self.stage <= 1 and self.micro_step > 0  # keep accumulating in place
+        for s in self.segments:
+            s.ready = 0
+            s.launched = False
+            for p in s.params:
+                if not accumulate_full:
+                    p._dtd_touched = False
+                p._dtd_pending = 0
+                p.grad = None
+        self._need_reset = False
+
+    def forward(self, *args, **kwargs):
+        if self._need_reset:
+            self._reset()
+        return self.module(*args, **kwargs)
+
+    def backward(self, loss: torch.Tensor) -> None:
+        if self.config.gas > 1:
+            loss = loss / self.config.gas
+        loss.backward()
+
+    def is_gradient_accumulation_boundary(self) -> bool:
+        return (self.micro_step + 1) % self.config.gas == 0
+
+    def step(self) -> None:
+        if not self.is_gradient_accumulation_boundary():
+            self.micro_step += 1
+            self._need_reset = True
+            return
+        if self.comm_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+        self.optimizer.step()
+        self._refresh_params()
+        self.micro_step = 0
+        self.global_steps += 1
+        self._need_reset = True
+        rt = getattr(self.module, "rt", None)
+        if rt is not None:
+            rt.rng.advance()
+
+    @torch.no_grad()
+    def _refresh_params(self) -> None:
+        """Stage 0: the kernel wrote the replicated params; stages 1-2: all-gather each
+        bucket from the updated shards; stage 3 units stay sharded until their next use."""
+        if self.stage == 0:
+            for s in self.buckets:
+                s.full.copy_(self.lowp_view[s.shard_off:s.shard_off + s.chunk])
+            return
+        for s in self.buckets:
+            src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
+            if self.world > 1:
+                with self._comm_ctx():
+                    w = clog.all_gather_into_tensor(s.full, src, group=self.group, async_op=True)
+                    w.wait()
+            else:
+                s.full.copy_(src)
+        if self.comm_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+
+    def zero_optimization_stage(self) -> int:
+        return self.stage
+
+    def train(self, mode: bool = True):
+        self.module.train(mode)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    # ------------------------------------------------------------------ introspection
+    def partition_numel(self) -> int:
+        return self.shard_numel
+
+    def state_bytes_per_rank(self) -> dict:
+        es = self.dtype.itemsize if hasattr(self.dtype, "itemsize") else torch.empty(0, dtype=self.dtype).element_size()
+        out = {"master_fp32": self.master.numel() * 4, "adam_moments": 2 * self.master.numel() * 4,
+               "grad_shard": self.gshard.numel() * self.gshard.element_size(),
+               "replicated_params": self.param_flat.numel() * es}
+        if self.grad_flat is not None:
+            out["full_grads"] = self.grad_flat.numel() * self.grad_flat.element_size()
+        return out
+
+
+def initialize(model: nn.Module, model_parameters=None, config: dict | None = None, optimizer=None, **_):
+    """DeepSpeed-compatible entry point: returns (engine, optimizer, None, None)."""
+    if optimizer is not None:
+        raise NotImplementedError("pass the optimizer through the config dict (type Adam/AdamW)")
+    engine = ZeroEngine(model, config, model_parameters)
+    return engine, engine.optimizer, None, None

@@ -1,0 +1,81 @@
+"""Worker functions for the multi-process CPU (gloo) tests; importable by spawned children."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from distributed_training_and_deepspeed_amd import comm  # noqa: E402
+from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset  # noqa: E402
+from distributed_training_and_deepspeed_amd.models import build_model  # noqa: E402
+
+
+def _batches(cfg, rank, world, n_steps, B=2, S=32, seed=7):
+    ds = SyntheticLMDataset(cfg, world * B * n_steps, seq_len=S, seed=seed)
+    ids = ds.input_ids.view(n_steps, world, B, S)
+    lab = ds.labels.view(n_steps, world, B, S)
+    return ids[:, rank], lab[:, rank]
+
+
+def ddp_worker(rank, world, port, out_dir, model_name, impl, n_steps, bucket_mb):
+    from distributed_training_and_deepspeed_amd.optim import hf_adamw
+    from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
+    comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
+    model = build_model(model_name, impl=impl, seed=3)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=bucket_mb)
+    opt = hf_adamw(ddp.parameters(), lr=1e-3)
+    ids, lab = _batches(model.cfg, rank, world, n_steps)
+    grads0 = None
+    for i in range(n_steps):
+        out = ddp(ids[i], labels=lab[i])
+        out.loss.backward()
+        if i == 0:
+            grads0 = {n: p.main_grad.detach().clone() for n, p in model.named_parameters()}
+        opt.step()
+        model.rt.rng.advance()
+    if rank == 0:
+        torch.save({"grads0": grads0, "params": {n: p.detach().clone() for n, p in model.named_parameters()},
+                    "buckets": ddp.bucket_sizes_bytes()}, os.path.join(out_dir, "ddp.pt"))
+    comm.destroy()
+
+
+def zero_worker(rank, world, port, out_dir, model_name, stage, n_steps, gas):
+    from distributed_training_and_deepspeed_amd.comm import logger as clog
+    from distributed_training_and_deepspeed_amd.parallel.zero import initialize
+    comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
+    model = build_model(model_name, impl="fused", seed=3)
+    cfg = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": gas,
+           "optimizer": {"type": "Adam", "params": {"lr": 1e-3}},
+           "comms_logger": {"enabled": True, "prof_all": True},
+           "zero_optimization": {"stage": stage, "reduce_bucket_size": 50000}}
+    eng, opt, _, _ = initialize(model=model, model_parameters=model.parameters(), config=cfg)
+    ids, lab = _batches(model.cfg, rank, world, n_steps * gas)
+    clog.comms_logger.reset()
+    for i in range(n_steps * gas):
+        loss = eng(ids[i], labels=lab[i]).loss
+        eng.backward(loss)
+        eng.step()
+    # gather full parameters (stage 3 keeps shards): reconstruct from every rank's master shard
+    shard = eng.master.detach().clone()
+    shards = [torch.zeros_like(shard) for _ in range(world)]
+    torch.distributed.all_gather(shards, shard)
+    if rank == 0:
+        torch.save({"shards": shards, "partition": eng.partition_numel(),
+                    "comms": {k: {s: v[0] for s, v in d.items()} for k, d in clog.comms_logger.comms_dict.items()},
+                    "layout": [(s.unit, s.numel, s.chunk, s.shard_off, s.shapes) for s in eng.segments]},
+                   os.path.join(out_dir, f"zero{stage}.pt"))
+    comm.destroy()
+
+
+def allreduce_worker(rank, world, port, out_dir):
+    sys.argv = ["x"]
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("pa", os.path.join(ROOT, "pytorch_allreduce.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    os.environ["MASTER_PORT"] = str(port)
+    t = mod.all_reduce_example(rank, world, "gloo")
+    torch.save(t, os.path.join(out_dir, f"ar{rank}.pt"))
