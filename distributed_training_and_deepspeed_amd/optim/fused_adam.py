@@ -139,6 +139,16 @@ class FusedAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        if self.gbuf is not None:  # gradients assigned to p.grad by hand (not via autograd)
+            for p in self._params:
+                g = p.grad
+                if g is not None and g.data_ptr() != p.main_grad.data_ptr():
+                    if getattr(p, "_dtd_touched", False):
+                        p.main_grad.add_(g.to(p.main_grad.dtype))
+                    else:
+                        p.main_grad.copy_(g)
+                    p._dtd_touched = True
+            self.gbuf.zero_untouched_()  # no gradient this step -> zero, not last step's value
         self._push_hparams()
         self.step_count += 1
         self.hp[5:6].add_(1.0)
