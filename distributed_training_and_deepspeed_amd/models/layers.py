@@ -93,14 +93,14 @@ class _EmbedFn(torch.autograd.Function):
             x, m, r = z, None, None
         out = Fx.dropout(x, p, rt.rng, sid)
         ctx.save_for_backward(ids, z, m, r)
-        ctx.mod, ctx.p, ctx.sid = mod, p, sid
+        ctx.mod, ctx.p, ctx.sid, ctx.rng = mod, p, sid, rt.rng
         return out.view(B, S, h)
 
     @staticmethod
     def backward(ctx, dout):
         ids, z, m, r = ctx.saved_tensors
         mod = ctx.mod
-        c, rng = mod.cfg, mod.rt.rng
+        c, rng = mod.cfg, ctx.rng
         B, S = ids.shape
         h = c.hidden_size
         dx = Fx.dropout(dout.reshape(B * S, h).contiguous(), ctx.p, rng, ctx.sid)
@@ -177,7 +177,8 @@ class _MLMHeadFn(torch.autograd.Function):
         c = head.cfg
         u = F.linear(x, head.dense_w, head.dense_b)
         a = Fx.act_fwd(u, c.activation)
-        _, t, m, r = Fx.ln_fwd(None, a, head.ln_g, head.ln_b, c.ln_eps, 0.0, head.rt.rng, 0)
+        ctx.rng = head.rt.rng
+        _, t, m, r = Fx.ln_fwd(None, a, head.ln_g, head.ln_b, c.ln_eps, 0.0, ctx.rng, 0)
         logits = F.linear(t, head.decoder_weight, head.decoder_bias)
         loss, lse, stats = Fx.xent_fwd(logits, labels)
         ctx.save_for_backward(x, labels, u, a, t, m, r, logits, lse, stats)
@@ -195,7 +196,7 @@ class _MLMHeadFn(torch.autograd.Function):
         grad_done(head.decoder_bias)
         emit_wgrad(head.decoder_weight, dlogits, t)
         dt = dlogits @ head.decoder_weight
-        da, _ = Fx.ln_bwd(dt, None, a, m, r, head.ln_g, 0.0, head.rt.rng, 0, want_dz=True,
+        da, _ = Fx.ln_bwd(dt, None, a, m, r, head.ln_g, 0.0, ctx.rng, 0, want_dz=True,
                           dgamma=grad_dst(head.ln_g), dbeta=grad_dst(head.ln_b))
         grad_done(head.ln_g)
         grad_done(head.ln_b)

@@ -193,13 +193,14 @@ class _FusedLayerFn(torch.autograd.Function):
         else:
             ctx.save_for_backward(x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3)
         ctx.layer = layer
+        ctx.rng = rng  # the RngState of this forward's device (pipeline stages differ)
         ctx.meta = (B, S, h, H, D, p_h, p_a, sa, s1, s2)
         return out.view(B, S, h)
 
     @staticmethod
     def backward(ctx, dout):
         layer = ctx.layer
-        c, rng = layer.cfg, layer.rt.rng
+        c, rng = layer.cfg, ctx.rng
         B, S, h, H, D, p_h, p_a, sa, s1, s2 = ctx.meta
         T = B * S
         (qkv_w, qkv_b, o_w, o_b, g1, b1, w1, bf1, w2, bf2, g2, b2) = layer.params()

@@ -18,3 +18,27 @@ def torch_adamw(params, lr: float = 5e-5, **kw) -> FusedAdam:
 def deepspeed_adam(params, lr: float = 1.5e-4, **kw) -> FusedAdam:
     """DeepSpeed "Adam" -> FusedAdam(adam_w_mode=True) defaults (zero_dp_training.py:28-33)."""
     return FusedAdam(params, lr=lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, adam_w_mode=True, **kw)
+
+
+class PerDeviceOptimizer:
+    """One fused optimizer per device for models spread over several GPUs (model/pipeline
+    parallelism): each device's parameters live in their own flat buffers."""
+
+    def __init__(self, params, factory, **kw):
+        groups = {}
+        for p in params:
+            if p.requires_grad:
+                groups.setdefault(str(p.device), []).append(p)
+        self.optimizers = [factory(ps, **kw) for ps in groups.values()]
+
+    @property
+    def param_groups(self):
+        return [g for o in self.optimizers for g in o.param_groups]
+
+    def step(self, closure=None):
+        for o in self.optimizers:
+            o.step()
+
+    def zero_grad(self, set_to_none: bool = True):
+        for o in self.optimizers:
+            o.zero_grad(set_to_none)

@@ -1,0 +1,178 @@
+"""Layer-wise model parallelism and GPipe pipelining across the GPUs of one process.
+
+Reference (model/bert_mp.py, model_parallel_training.py):
+* naive placement: the flat module list is split into contiguous groups with the
+  ``np.array_split`` law (first ``n % d`` groups one longer) and group i lives on device i;
+* forward moves activations between groups; only one device works at a time, which the
+  per-device idle-time table makes visible;
+* ``to_pipeline(chunks)`` wraps the stages in torch's GPipe ``Pipe`` (removed from torch >= 2.4):
+  fill-drain schedule over ``chunks`` micro-batches, activation checkpointing of every
+  micro-batch except the last, copy streams between devices.
+
+Here: ``GPipe`` issues micro-batch m of stage s at clock t = m + s from one Python thread;
+kernel launches are asynchronous per device, so stage s computes micro-batch m while stage
+s-1 already runs m+1 (the same overlap torch Pipe gets from per-device worker threads), and
+activations move on side copy streams (``parallel/p2p.py``).  Checkpointed micro-batches are
+recomputed in backward with *identical* dropout masks, because masks come from the counter
+RNG keyed on the micro-batch index (``RngState.micro``) rather than from a saved RNG state.
+``IdleTimeTracker`` measures per-device idle gaps with HIP events on each device's stream
+(device-accurate) or, like the reference, with host timestamps.
+"""
+from __future__ import annotations
+
+import time
+from datetime import datetime
+
+import torch
+from torch import nn
+from torch.utils.checkpoint import checkpoint
+
+from .p2p import send_to
+
+
+def array_split_sizes(n: int, parts: int) -> list[int]:
+    """Group sizes of ``np.array_split(range(n), parts)``."""
+    q, r = divmod(n, parts)
+    return [q + 1 if i < r else q for i in range(parts)]
+
+
+def partition(modules: list, parts: int) -> list[list]:
+    out, i = [], 0
+    for sz in array_split_sizes(len(modules), parts):
+        out.append(modules[i:i + sz])
+        i += sz
+    return out
+
+
+class IdleTimeTracker:
+    """Per-device idle time between consecutive forward/backward activities.
+
+    ``timing='device'``: HIP events recorded on the device's current stream at group entry and
+    exit; idle = event gap from a device's previous exit to its next entry (resolved at
+    ``collect()``).  ``timing='host'``: ``time.time()`` like the reference hooks
+    (model/bert_mp.py:106-130).  ``device_idle_time[d] = (sum_ms, count)``."""
+
+    def __init__(self, devices, timing: str = "device", verbose: bool = False):
+        self.devices = list(devices)
+        self.timing = timing if any(torch.device(d).type == "cuda" for d in self.devices) else "host"
+        self.verbose = verbose
+        self.device_idle_time = {i: (0.0, 0) for i in range(len(self.devices))}
+        self._last = {}
+        self._pending = []
+
+    def _stamp(self, idx: int):
+        if self.timing == "host":
+            return time.time()
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(torch.device(self.devices[idx])))
+        return ev
+
+    def mark(self, idx: int, forward: bool, entering: bool) -> None:
+        now = self._stamp(idx)
+        last = self._last.get(idx)
+        msg = f"{'Entering' if entering else 'Finished'} {'forward' if forward else 'backward'} pass on device {idx}"
+        if entering and last is not None:
+            if self.timing == "host":
+                ms = (now - last) * 1000.0
+                self._add(idx, ms)
+                msg += f". Idle time: {ms:.2f}ms"
+            else:
+                self._pending.append((idx, last, now))
+        self._last[idx] = now
+        if self.verbose:
+            print(f"{datetime.now()} - {msg}")
+
+    def _add(self, idx: int, ms: float) -> None:
+        s, c = self.device_idle_time[idx]
+        self.device_idle_time[idx] = (s + ms, c + 1)
+
+    def collect(self) -> None:
+        if not self._pending:
+            return
+        torch.cuda.synchronize()
+        for idx, a, b in self._pending:
+            self._add(idx, max(0.0, a.elapsed_time(b)))
+        self._pending = []
+
+    def step_boundary(self) -> None:
+        """Idle time is accumulated within a training step (not across optimizer steps)."""
+        self.collect()
+        self._last = {}
+
+    def table(self, steps: int) -> list[list]:
+        self.collect()
+        rows = [["Device", "Average Idle Time (ms)"]]
+        for k, (s, _) in self.device_idle_time.items():
+            rows.append([k, s / max(steps, 1)])
+        return rows
+
+
+def attach_idle_hooks(groups: list[list[nn.Module]], tracker: IdleTimeTracker) -> None:
+    """Forward pre/post hooks and full-backward pre/post hooks on each group's boundary modules.
+    (The reference registers its 'entering forward' hook as a post-hook on the group's first
+    module -- quirk 6; the pre-hook here measures from the true group entry.)"""
+    for idx, g in enumerate(groups):
+        first, last = g[0], g[-1]
+        first.register_forward_pre_hook(lambda m, a, i=idx: tracker.mark(i, True, True))
+        last.register_forward_hook(lambda m, a, o, i=idx: tracker.mark(i, True, False))
+        last.register_full_backward_pre_hook(lambda m, go, i=idx: tracker.mark(i, False, True))
+        first.register_full_backward_hook(lambda m, gi, go, i=idx: tracker.mark(i, False, False))
+
+
+class GPipe(nn.Module):
+    """Synchronous pipeline (fill-drain) over per-device stages.
+
+    stages[i] is an nn.Module (usually nn.Sequential) resident on devices[i].  ``chunks``
+    micro-batches are split along dim 0.  ``checkpoint``: 'except_last' (torch Pipe default),
+    'always' or 'never'.  ``set_micro(m)`` (optional) is called before each micro-batch's
+    forward and recompute so dropout masks are keyed on the micro-batch."""
+
+    def __init__(self, stages, devices, chunks: int = 1, checkpoint: str = "except_last", set_micro=None,
+                 owner: nn.Module | None = None):
+        super().__init__()
+        self.stages = nn.ModuleList(stages)
+        self.owner = owner  # the full model: makes .parameters() / .train() cover every stage
+        self.devices = [torch.device(d) for d in devices]
+        self.chunks = chunks
+        self.checkpoint = checkpoint
+        self.set_micro = set_micro
+
+    def _run(self, s: int, m: int, x):
+        def fn(inp, _s=s, _m=m):
+            if self.set_micro is not None:
+                self.set_micro(_m)
+            return self.stages[_s](inp)
+        ck = (self.checkpoint == "always") or (self.checkpoint == "except_last" and m < self.chunks - 1)
+        if ck and torch.is_grad_enabled() and self.training:
+            return checkpoint(fn, x, use_reentrant=False, preserve_rng_state=False)
+        return fn(x)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        micro = list(torch.chunk(x, self.chunks, dim=0))
+        n, S = len(micro), len(self.stages)
+        acts = [[None] * n for _ in range(S)]
+        for clock in range(n + S - 1):
+            for s in range(S):
+                m = clock - s
+                if not 0 <= m < n:
+                    continue
+                inp = micro[m] if s == 0 else acts[s - 1][m]
+                inp = send_to(inp, self.devices[s]) if torch.is_tensor(inp) else inp
+                with torch.cuda.device(self.devices[s]) if self.devices[s].type == "cuda" else _null():
+                    acts[s][m] = self._run(s, m, inp)
+                if s > 0:
+                    acts[s - 1][m] = None
+        if self.set_micro is not None:
+            self.set_micro(0)
+        return torch.cat(acts[S - 1], dim=0)
+
+    def local_value(self):  # torch Pipe returned an RRef; kept for script-level parity
+        return self
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
