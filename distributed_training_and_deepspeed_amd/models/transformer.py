@@ -174,7 +174,7 @@ class _FusedLayerFn(torch.autograd.Function):
         else:
             a_in = x2d
         qkv = F.linear(a_in, qkv_w, qkv_b)
-        actx, lse = A.attn_fwd(qkv, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa)
+        actx, lse, amask = A.attn_fwd(qkv, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa)
         o = F.linear(actx, o_w, o_b)
         if c.pre_ln:
             z1, f_in, m2, r2 = Fx.ln_fwd(o, x2d, g2, b2, eps, p_h, rng, s1)
@@ -193,6 +193,7 @@ class _FusedLayerFn(torch.autograd.Function):
         else:
             ctx.save_for_backward(x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3)
         ctx.layer = layer
+        ctx.amask = amask  # attention dropout keep bits (kernel path) for the backward
         ctx.rng = rng  # the RngState of this forward's device (pipeline stages differ)
         ctx.meta = (B, S, h, H, D, p_h, p_a, sa, s1, s2)
         return out.view(B, S, h)
@@ -240,7 +241,7 @@ class _FusedLayerFn(torch.autograd.Function):
                 grad_done(p)
         emit_wgrad(o_w, do, actx)
         dctx = do @ o_w
-        dqkv = A.attn_bwd(dctx, qkv, actx, lse, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa)
+        dqkv = A.attn_bwd(dctx, qkv, actx, lse, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, ctx.amask)
         Fx.bias_grad(dqkv, *_pair(qkv_b))
         grad_done(qkv_b)
         if c.pre_ln:

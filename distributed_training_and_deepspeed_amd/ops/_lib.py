@@ -53,8 +53,8 @@ _SIGS = {
     "dtd_sqnorm_num_partials": (I, [SZ]),
     "dtd_sqnorm_partials": (I, [P, I, SZ, P, P]),
     # attention.hip
-    "dtd_attn_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, F, F, P, U32, P]),
-    "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, F, F, P, U32, P]),
+    "dtd_attn_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, U32, P]),
+    "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
 }
 
 

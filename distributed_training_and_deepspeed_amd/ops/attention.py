@@ -108,26 +108,32 @@ def kernel_supported(qkv: torch.Tensor, D: int) -> bool:
 
 
 def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | None = None, sid=0):
-    """Returns (ctx [B*S, H*D], lse [B, H, S] fp32)."""
+    """Returns (ctx [B*S, H*D], lse [B, H, S] fp32, masks).  ``masks`` holds the dropout keep
+    bits for the backward ([2, B*H*S*ceil(S/32)] int32 on the kernel path, None otherwise)."""
     if not kernel_supported(qkv, D):
         if qkv.is_cuda and qkv.dtype == torch.bfloat16 and _lib.has("dtd_attn_fwd") is False:
             _warn_once()
-        return attn_fwd_ref(qkv, B, S, H, D, causal, slopes, p, rng, sid)
+        ctx, lse = attn_fwd_ref(qkv, B, S, H, D, causal, slopes, p, rng, sid)
+        return ctx, lse, None
     qkv = qkv.contiguous()
     ctx = torch.empty((B * S, H * D), dtype=qkv.dtype, device=qkv.device)
     lse = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+    masks = None
+    if p > 0:
+        W = (S + 31) // 32
+        masks = torch.empty((2, B * H * S * W), dtype=torch.int32, device=qkv.device)
     sl = slopes.to(device=qkv.device, dtype=torch.float32).contiguous() if slopes is not None else None
     # q/k/v are strided views into qkv: row stride 3*H*D, head stride D.
     ld = 3 * H * D
     base = qkv.data_ptr()
     es = qkv.element_size()
     _lib.call("dtd_attn_fwd", base, base + H * D * es, base + 2 * H * D * es, ctx.data_ptr(), lse.data_ptr(),
-              _lib.ptr(sl), B, S, H, D, ld, H * D, int(causal), 0, 0, 1.0 / math.sqrt(D), float(p),
+              _lib.ptr(sl), _lib.ptr(masks), B, S, H, D, ld, H * D, int(causal), 1.0 / math.sqrt(D), float(p),
               rng.state.data_ptr() if rng is not None else None, sid, _lib.stream())
-    return ctx, lse
+    return ctx, lse, masks
 
 
-def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, rng=None, sid=0):
+def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, rng=None, sid=0, masks=None):
     """Returns dqkv [B*S, 3*H*D] in the qkv layout."""
     if not kernel_supported(qkv, D):
         return attn_bwd_ref(dctx, qkv, ctx, lse, B, S, H, D, causal, slopes, p, rng, sid)
@@ -139,7 +145,6 @@ def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, 
     es = qkv.element_size()
     qb, gb = qkv.data_ptr(), dqkv.data_ptr()
     _lib.call("dtd_attn_bwd", qb, qb + H * D * es, qb + 2 * H * D * es, ctx.data_ptr(), dctx.data_ptr(),
-              lse.data_ptr(), delta.data_ptr(), None, gb, gb + H * D * es, gb + 2 * H * D * es,
-              _lib.ptr(sl), B, S, H, D, ld, H * D, int(causal), 0, 0, 1.0 / math.sqrt(D), float(p),
-              rng.state.data_ptr() if rng is not None else None, sid, _lib.stream())
+              lse.data_ptr(), delta.data_ptr(), _lib.ptr(masks), gb, gb + H * D * es, gb + 2 * H * D * es,
+              _lib.ptr(sl), B, S, H, D, ld, H * D, int(causal), 1.0 / math.sqrt(D), float(p), _lib.stream())
     return dqkv

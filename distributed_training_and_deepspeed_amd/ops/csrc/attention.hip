@@ -75,9 +75,59 @@ __device__ __forceinline__ float keep_of(const DropoutRng& g, uint64_t e, uint32
 
 struct FwdArgs {
   const bf16* q; const bf16* k; const bf16* v; bf16* o; float* lse; const float* slopes;
-  int B, S, H, ld, ldo, causal;
-  float scale, p; const uint64_t* rng; uint32_t sid;
+  const uint32_t* maskA;  // dropout keep bits [B*H][S][W]: bit j of word w = key 32w+j  (nullptr: no dropout)
+  int B, S, H, ld, ldo, causal, W;
+  float scale, p;
 };
+
+// Dropout keep-masks for one attention call, generated once in a VALU-only pass at full
+// occupancy (instead of re-hashing inside the MFMA-bound forward, dK/dV and dQ kernels) and
+// stored as bits in two layouts so every consumer reads ONE 32-bit word per 32x32 tile:
+//   A [bh][q][w]  : bit j = key 32w+j   (forward / dQ: query on the lane)
+//   B [bh][key][w]: bit j = q   32w+j   (dK/dV: key on the lane) -- the transpose of A, formed
+//                   with wave ballots.
+// Keep(bh, q, key) = counter-RNG decision for flat element ((bh*S + q)*S + key), identical to
+// ops/rng.py keep_mask (so the math reference reproduces the masks bit for bit).
+// grid: (ceil(S/32), ceil(S/64), B*H); block: 64 = 32 queries x 2 key-words.
+__global__ void __launch_bounds__(64) attn_mask_kernel(uint32_t* __restrict__ maskA, uint32_t* __restrict__ maskB, int S,
+                                                       int W, const uint64_t* rng, uint32_t sid, uint32_t thr) {
+  DropoutRng g(rng, sid);
+  const int lane = threadIdx.x, bh = blockIdx.z;
+  const int q = blockIdx.x * 32 + (lane & 31);
+  const int kw = blockIdx.y * 2 + (lane >> 5);
+  uint32_t word = 0;
+  if (q < S && kw < W) {
+    const uint64_t base = ((uint64_t)bh * S + (uint64_t)q) * (uint64_t)S + (uint64_t)kw * 32;
+    const int nk = min(32, S - kw * 32);
+    if ((base & 1) == 0) {
+#pragma unroll 4
+      for (int j = 0; j < 32; j += 2) {
+        const uint32_t b = g.bits((base + j) >> 1);
+        word |= (uint32_t)((b & 0xffffu) >= thr) << j;
+        word |= (uint32_t)((b >> 16) >= thr) << (j + 1);
+      }
+    } else {
+      for (int j = 0; j < 32; ++j) {
+        const uint64_t e = base + j;
+        const uint32_t b = g.bits(e >> 1);
+        const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
+        word |= (uint32_t)(h16 >= thr) << j;
+      }
+    }
+    if (nk < 32) word &= (nk > 0 ? (0xffffffffu >> (32 - nk)) : 0u);
+    maskA[((size_t)bh * S + q) * W + kw] = word;
+  }
+  // transpose through ballots: bit j of lane l's word -> word for key (kw*32 + j), q-block x
+#pragma unroll 4
+  for (int j = 0; j < 32; ++j) {
+    const unsigned long long bal = __ballot((word >> j) & 1u);
+    if (lane == 0) {
+      const int k0 = blockIdx.y * 64 + j, k1 = k0 + 32;
+      if (k0 < S) maskB[((size_t)bh * S + k0) * W + blockIdx.x] = (uint32_t)bal;
+      if (k1 < S) maskB[((size_t)bh * S + k1) * W + blockIdx.x] = (uint32_t)(bal >> 32);
+    }
+  }
+}
 
 // Stage a [rows x D] bf16 tile (row stride `ld` in global) into registers, then LDS.
 template <int D, int ROWS>
@@ -120,10 +170,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(FwdArgs a) {
   const bool qvalid = q < S;
   const float sl2 = a.slopes ? a.slopes[h] * kLog2e : 0.f;
   const float sc2 = a.scale * kLog2e;
-  const bool drop = a.p > 0.f;
-  DropoutRng g(a.rng, a.sid);
-  const uint32_t thr = keep_threshold(a.p);
+  const bool drop = a.maskA != nullptr;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
+  const uint32_t* mrow = drop ? a.maskA + ((size_t)bh * S + (qvalid ? q : 0)) * a.W : nullptr;
   const bf16* kbase = a.k + (size_t)b * S * a.ld + h * D;
   const bf16* vbase = a.v + (size_t)b * S * a.ld + h * D;
 
@@ -137,7 +186,6 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(FwdArgs a) {
 #pragma unroll
   for (int d = 0; d < NDB; ++d) oacc[d] = f32x16{};
   float m = -INFINITY, l = 0.f;
-  const uint64_t rowbase = ((uint64_t)bh * S + (uint64_t)(qvalid ? q : 0)) * (uint64_t)S;
 
   const int kend = a.causal ? min(S, qblk + 128) : S;
   const int nt = (kend + BN - 1) / BN;
@@ -194,19 +242,12 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(FwdArgs a) {
     }
     if (drop) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb) {
+        const int kw = (k0 >> 5) + kb;
+        const uint32_t mw = kw < a.W ? mrow[kw] : 0u;
 #pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const uint64_t e = rowbase + (uint64_t)(k0 + kb * 32 + crow(i, hh));
-          if ((e & 1) == 0) {  // (e, e+1) share one hash
-            const uint32_t bits = g.bits(e >> 1);
-            sacc[kb][i] *= ((bits & 0xffffu) >= thr) ? inv_keep : 0.f;
-            sacc[kb][i + 1] *= ((bits >> 16) >= thr) ? inv_keep : 0.f;
-          } else {
-            sacc[kb][i] *= keep_of(g, e, thr) * inv_keep;
-            sacc[kb][i + 1] *= keep_of(g, e + 1, thr) * inv_keep;
-          }
-        }
+        for (int i = 0; i < 16; ++i) sacc[kb][i] *= ((mw >> crow(i, hh)) & 1u) ? inv_keep : 0.f;
+      }
     }
     // O^T += V^T . P^T: the score accumulator is the B operand; V^T comes from transposed reads
 #pragma unroll
@@ -257,8 +298,9 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const bf16* __restr
 struct BwdArgs {
   const bf16* q; const bf16* k; const bf16* v; const bf16* dout; const float* lse; const float* delta;
   bf16* dq; bf16* dk; bf16* dv; const float* slopes;
-  int B, S, H, ld, ldo, causal;
-  float scale, p; const uint64_t* rng; uint32_t sid;
+  const uint32_t* maskA; const uint32_t* maskB;  // dropout keep bits (see attn_mask_kernel)
+  int B, S, H, ld, ldo, causal, W;
+  float scale, p;
 };
 
 // dK, dV: grid (ceil(S/128), B*H); block 256 = 4 waves x 32 keys ("key on the lane").
@@ -278,10 +320,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(BwdArgs a) {
   const bool kvalid = key < S;
   const float sl2 = a.slopes ? a.slopes[h] * kLog2e : 0.f;
   const float sc2 = a.scale * kLog2e;
-  const bool drop = a.p > 0.f;
-  DropoutRng g(a.rng, a.sid);
-  const uint32_t thr = keep_threshold(a.p);
+  const bool drop = a.maskB != nullptr;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
+  const uint32_t* mrow = drop ? a.maskB + ((size_t)bh * S + (kvalid ? key : 0)) * a.W : nullptr;
   const bf16* qbase = a.q + (size_t)b * S * a.ld + h * D;
   const bf16* obase = a.dout + (size_t)b * S * a.ldo + h * D;
   const float* lseb = a.lse + (size_t)bh * S;
@@ -333,6 +374,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(BwdArgs a) {
       }
       const int qrow0 = q0 + qb * 32;
       const bool needmask = !kvalid || (qrow0 + 32 > S) || (a.causal && key > qrow0);
+      const uint32_t mw = drop && (qrow0 >> 5) < a.W ? mrow[qrow0 >> 5] : 0u;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qr = qb * 32 + crow(i, hh);
@@ -340,8 +382,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(BwdArgs a) {
         const float s = fmaf(sacc[i], sc2, sl2 * (float)key - lse_s[buf][qr]);
         float pv = exp2f(s);
         if (needmask && (!kvalid || qq >= S || (a.causal && key > qq))) pv = 0.f;
-        float keep = 1.f;
-        if (drop) keep = keep_of(g, ((uint64_t)bh * S + (uint64_t)qq) * (uint64_t)S + key, thr) * inv_keep;
+        const float keep = drop ? (((mw >> crow(i, hh)) & 1u) ? inv_keep : 0.f) : 1.f;
         sacc[i] = pv * keep;                                  // dropped P (for dV)
         pacc[i] = pv * (pacc[i] * keep - del_s[buf][qr]);     // dS
       }
@@ -396,10 +437,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(BwdArgs a) {
   const bool qvalid = q < S;
   const float sl2 = a.slopes ? a.slopes[h] * kLog2e : 0.f;
   const float sc2 = a.scale * kLog2e;
-  const bool drop = a.p > 0.f;
-  DropoutRng g(a.rng, a.sid);
-  const uint32_t thr = keep_threshold(a.p);
+  const bool drop = a.maskA != nullptr;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
+  const uint32_t* mrow = drop ? a.maskA + ((size_t)bh * S + (qvalid ? q : 0)) * a.W : nullptr;
   const bf16* kbase = a.k + (size_t)b * S * a.ld + h * D;
   const bf16* vbase = a.v + (size_t)b * S * a.ld + h * D;
 
@@ -415,7 +455,6 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(BwdArgs a) {
   }
   const float lse2 = qvalid ? a.lse[(size_t)bh * S + q] * kLog2e : 0.f;
   const float dl = qvalid ? a.delta[(size_t)bh * S + q] : 0.f;
-  const uint64_t rowbase = ((uint64_t)bh * S + (uint64_t)(qvalid ? q : 0)) * (uint64_t)S;
   f32x16 dq[NDB];
 #pragma unroll
   for (int d = 0; d < NDB; ++d) dq[d] = f32x16{};
@@ -442,13 +481,14 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(BwdArgs a) {
         sacc = mfma32(*reinterpret_cast<const bf16x8*>(&K[(kb * 32 + r) * KP + 16 * c + 8 * hh]), qf[c], sacc);
         pacc = mfma32(*reinterpret_cast<const bf16x8*>(&V[(kb * 32 + r) * KP + 16 * c + 8 * hh]), of[c], pacc);
       }
+      const int kw = (k0 >> 5) + kb;
+      const uint32_t mw = drop && kw < a.W ? mrow[kw] : 0u;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int key = k0 + kb * 32 + crow(i, hh);
         float pv = exp2f(fmaf(sacc[i], sc2, sl2 * (float)key - lse2));
         if (needmask && (!qvalid || key >= S || (a.causal && key > q))) pv = 0.f;
-        float keep = 1.f;
-        if (drop) keep = keep_of(g, rowbase + (uint64_t)key, thr) * inv_keep;
+        const float keep = drop ? (((mw >> crow(i, hh)) & 1u) ? inv_keep : 0.f) : 1.f;
         sacc[i] = pv * (pacc[i] * keep - dl);  // dS^T
       }
 #pragma unroll
@@ -479,13 +519,22 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(BwdArgs a) {
 }  // namespace
 
 // q,k,v,o: bf16 views with row stride ld (q/k/v) / ldo (o); lse: [B,H,S] fp32.
+// masks: [2][B*H*S*W] uint32 (W = ceil(S/32)) written here when p > 0 (read by the backward).
 DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const float* slopes,
-                            int B, int S, int H, int D, int ld, int ldo, int causal, int r0, int r1, float scale,
+                            uint32_t* masks, int B, int S, int H, int D, int ld, int ldo, int causal, float scale,
                             float p, const uint64_t* rng, uint32_t sid, hipStream_t s) {
-  (void)r0; (void)r1;
   if (B * S * H == 0) return 0;
-  FwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, slopes, B, S, H, ld, ldo, causal,
-            scale, p, rng, sid};
+  const int W = (S + 31) / 32;
+  uint32_t* mA = nullptr;
+  if (p > 0.f) {
+    if (!masks) return (int)hipErrorInvalidValue;
+    mA = masks;
+    uint32_t* mB = masks + (size_t)B * H * S * W;
+    hipLaunchKernelGGL(attn_mask_kernel, dim3(W, (S + 63) / 64, B * H), dim3(64), 0, s, mA, mB, S, W, rng, sid,
+                       keep_threshold(p));
+  }
+  FwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, slopes, mA, B, S, H, ld, ldo, causal, W,
+            scale, p};
   dim3 grid((S + 127) / 128, B * H);
   if (D == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, a);
   else if (D == 128) hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, s, a);
@@ -495,15 +544,18 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
 
 // dq/dk/dv: bf16 views with row stride ld into dqkv.  `delta` is [B,H,S] fp32 scratch.
 DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
-                            const float* lse, float* delta, float* unused, void* dq, void* dk, void* dv,
-                            const float* slopes, int B, int S, int H, int D, int ld, int ldo, int causal, int r0,
-                            int r1, float scale, float p, const uint64_t* rng, uint32_t sid, hipStream_t s) {
-  (void)r0; (void)r1; (void)unused;
+                            const float* lse, float* delta, const uint32_t* masks, void* dq, void* dk, void* dv,
+                            const float* slopes, int B, int S, int H, int D, int ld, int ldo, int causal, float scale,
+                            float p, hipStream_t s) {
   if (B * S * H == 0) return 0;
   if (D != 64 && D != 128) return (int)hipErrorInvalidValue;
+  const int W = (S + 31) / 32;
+  const uint32_t* mA = (p > 0.f) ? masks : nullptr;
+  const uint32_t* mB = (p > 0.f) ? masks + (size_t)B * H * S * W : nullptr;
+  if (p > 0.f && !masks) return (int)hipErrorInvalidValue;
   dim3 grid((S + 127) / 128, B * H);
   BwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, (bf16*)dk,
-            (bf16*)dv, slopes, B, S, H, ld, ldo, causal, scale, p, rng, sid};
+            (bf16*)dv, slopes, mA, mB, B, S, H, ld, ldo, causal, W, scale, p};
   if (D == 64) {
     hipLaunchKernelGGL(attn_bwd_delta_kernel<64>, dim3(B * S), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<64>, grid, dim3(256), 0, s, a);

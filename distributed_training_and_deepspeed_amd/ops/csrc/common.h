@@ -179,7 +179,7 @@ struct DropoutRng {
   }
 };
 // Two keep-decisions per 32 random bits (16-bit thresholds: p quantised to 1/65536).
-__device__ __forceinline__ uint32_t keep_threshold(float p) {
+__host__ __device__ __forceinline__ uint32_t keep_threshold(float p) {
   float t = p * 65536.0f;
   return t >= 65536.0f ? 65536u : (uint32_t)(t + 0.5f);
 }

@@ -38,11 +38,11 @@ def test_flash_attention_fwd_bwd(B, S, H, D, causal, alibi, p):
     slopes = A.alibi_slopes(H) if alibi else None
     rg, rc = RngState(11, device="cuda"), RngState(11, device="cpu")
     assert A.kernel_supported(qkv.cuda(), D)
-    ctx_g, lse_g = A.attn_fwd(qkv.cuda(), B, S, H, D, causal, slopes, p, rg, 9)
+    ctx_g, lse_g, mk = A.attn_fwd(qkv.cuda(), B, S, H, D, causal, slopes, p, rg, 9)
     ctx_r, lse_r = A.attn_fwd_ref(qkv, B, S, H, D, causal, slopes, p, rc, 9)
     assert rel(ctx_g, ctx_r) < 1e-2, rel(ctx_g, ctx_r)
     assert (lse_g.cpu() - lse_r).abs().max().item() < 2e-2
-    dq_g = A.attn_bwd(dctx.cuda(), qkv.cuda(), ctx_g, lse_g, B, S, H, D, causal, slopes, p, rg, 9)
+    dq_g = A.attn_bwd(dctx.cuda(), qkv.cuda(), ctx_g, lse_g, B, S, H, D, causal, slopes, p, rg, 9, mk)
     dq_r = A.attn_bwd_ref(dctx, qkv, ctx_r, lse_r, B, S, H, D, causal, slopes, p, rc, 9)
     g = dq_g.view(B, S, 3, H, D).cpu()
     r = dq_r.view(B, S, 3, H, D)
