@@ -117,16 +117,17 @@ __global__ void __launch_bounds__(64) attn_mask_kernel(uint32_t* __restrict__ ma
     if (nk < 32) word &= (nk > 0 ? (0xffffffffu >> (32 - nk)) : 0u);
     maskA[((size_t)bh * S + q) * W + kw] = word;
   }
-  // transpose through ballots: bit j of lane l's word -> word for key (kw*32 + j), q-block x
-#pragma unroll 4
+  // transpose through ballots: ballot j holds, for key-words kw0 (low half) and kw0+1 (high
+  // half), the q-bits of key 32*kw + j.  Lane j keeps the low word, lane 32+j the high word, so
+  // the 64 B-words leave in ONE store instruction.
+  uint32_t mine = 0;
+#pragma unroll
   for (int j = 0; j < 32; ++j) {
     const unsigned long long bal = __ballot((word >> j) & 1u);
-    if (lane == 0) {
-      const int k0 = blockIdx.y * 64 + j, k1 = k0 + 32;
-      if (k0 < S) maskB[((size_t)bh * S + k0) * W + blockIdx.x] = (uint32_t)bal;
-      if (k1 < S) maskB[((size_t)bh * S + k1) * W + blockIdx.x] = (uint32_t)(bal >> 32);
-    }
+    if ((lane & 31) == j) mine = (lane < 32) ? (uint32_t)bal : (uint32_t)(bal >> 32);
   }
+  const int key = blockIdx.y * 64 + lane;  // lane < 32: key-word kw0, lane >= 32: kw0 + 1
+  if (key < S) maskB[((size_t)bh * S + key) * W + blockIdx.x] = mine;
 }
 
 // Stage a [rows x D] bf16 tile (row stride `ld` in global) into registers, then LDS.
