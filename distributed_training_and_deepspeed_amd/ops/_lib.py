@@ -55,6 +55,8 @@ _SIGS = {
     # attention.hip
     "dtd_attn_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, U32, P]),
     "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
+    # reduce.hip
+    "dtd_splitk_reduce": (I, [P, I, I, ctypes.c_longlong, P, I, I, P]),
 }
 
 

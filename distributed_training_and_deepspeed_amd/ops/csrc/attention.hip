@@ -75,7 +75,7 @@ __device__ __forceinline__ float keep_of(const DropoutRng& g, uint64_t e, uint32
 
 struct FwdArgs {
   const bf16* q; const bf16* k; const bf16* v; bf16* o; float* lse; const float* slopes;
-  const uint32_t* maskA;  // dropout keep bits [B*H][S][W]: bit j of word w = key 32w+j  (nullptr: no dropout)
+  const uint32_t* maskA;  // dropout keep bits [B*H][W][S]: bit j of word (w, q) = key 32w+j  (nullptr: no dropout)
   int B, S, H, ld, ldo, causal, W;
   float scale, p;
 };
@@ -83,9 +83,12 @@ struct FwdArgs {
 // Dropout keep-masks for one attention call, generated once in a VALU-only pass at full
 // occupancy (instead of re-hashing inside the MFMA-bound forward, dK/dV and dQ kernels) and
 // stored as bits in two layouts so every consumer reads ONE 32-bit word per 32x32 tile:
-//   A [bh][q][w]  : bit j = key 32w+j   (forward / dQ: query on the lane)
-//   B [bh][key][w]: bit j = q   32w+j   (dK/dV: key on the lane) -- the transpose of A, formed
+//   A [bh][w][q]  : bit j = key 32w+j   (forward / dQ: query on the lane)
+//   B [bh][w][key]: bit j = q   32w+j   (dK/dV: key on the lane) -- the transpose of A, formed
 //                   with wave ballots.
+// Word-major ([w] outside the position) so that the 64 lanes of a consumer wave, which own 64
+// consecutive queries (keys), load one contiguous 256 B line per tile -- and the generator's
+// stores are contiguous too.
 // Keep(bh, q, key) = counter-RNG decision for flat element ((bh*S + q)*S + key), identical to
 // ops/rng.py keep_mask (so the math reference reproduces the masks bit for bit).
 // grid: (ceil(S/32), ceil(S/64), B*H); block: 64 = 32 queries x 2 key-words.
@@ -115,7 +118,7 @@ __global__ void __launch_bounds__(64) attn_mask_kernel(uint32_t* __restrict__ ma
       }
     }
     if (nk < 32) word &= (nk > 0 ? (0xffffffffu >> (32 - nk)) : 0u);
-    maskA[((size_t)bh * S + q) * W + kw] = word;
+    maskA[((size_t)bh * W + kw) * S + q] = word;
   }
   // transpose through ballots: ballot j holds, for key-words kw0 (low half) and kw0+1 (high
   // half), the q-bits of key 32*kw + j.  Lane j keeps the low word, lane 32+j the high word, so
@@ -127,7 +130,7 @@ __global__ void __launch_bounds__(64) attn_mask_kernel(uint32_t* __restrict__ ma
     if ((lane & 31) == j) mine = (lane < 32) ? (uint32_t)bal : (uint32_t)(bal >> 32);
   }
   const int key = blockIdx.y * 64 + lane;  // lane < 32: key-word kw0, lane >= 32: kw0 + 1
-  if (key < S) maskB[((size_t)bh * S + key) * W + blockIdx.x] = mine;
+  if (key < S) maskB[((size_t)bh * W + blockIdx.x) * S + key] = mine;
 }
 
 // Stage a [rows x D] bf16 tile (row stride `ld` in global) into registers, then LDS.
@@ -173,7 +176,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(FwdArgs a) {
   const float sc2 = a.scale * kLog2e;
   const bool drop = a.maskA != nullptr;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
-  const uint32_t* mrow = drop ? a.maskA + ((size_t)bh * S + (qvalid ? q : 0)) * a.W : nullptr;
+  const uint32_t* mcol = drop ? a.maskA + (size_t)bh * a.W * S + (qvalid ? q : 0) : nullptr;
   const bf16* kbase = a.k + (size_t)b * S * a.ld + h * D;
   const bf16* vbase = a.v + (size_t)b * S * a.ld + h * D;
 
@@ -245,7 +248,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         const int kw = (k0 >> 5) + kb;
-        const uint32_t mw = kw < a.W ? mrow[kw] : 0u;
+        const uint32_t mw = kw < a.W ? mcol[(size_t)kw * S] : 0u;
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[kb][i] *= ((mw >> crow(i, hh)) & 1u) ? inv_keep : 0.f;
       }
@@ -323,7 +326,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(BwdArgs a) {
   const float sc2 = a.scale * kLog2e;
   const bool drop = a.maskB != nullptr;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
-  const uint32_t* mrow = drop ? a.maskB + ((size_t)bh * S + (kvalid ? key : 0)) * a.W : nullptr;
+  const uint32_t* mcol = drop ? a.maskB + (size_t)bh * a.W * S + (kvalid ? key : 0) : nullptr;
   const bf16* qbase = a.q + (size_t)b * S * a.ld + h * D;
   const bf16* obase = a.dout + (size_t)b * S * a.ldo + h * D;
   const float* lseb = a.lse + (size_t)bh * S;
@@ -375,7 +378,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(BwdArgs a) {
       }
       const int qrow0 = q0 + qb * 32;
       const bool needmask = !kvalid || (qrow0 + 32 > S) || (a.causal && key > qrow0);
-      const uint32_t mw = drop && (qrow0 >> 5) < a.W ? mrow[qrow0 >> 5] : 0u;
+      const uint32_t mw = drop && (qrow0 >> 5) < a.W ? mcol[(size_t)(qrow0 >> 5) * S] : 0u;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qr = qb * 32 + crow(i, hh);
@@ -440,7 +443,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(BwdArgs a) {
   const float sc2 = a.scale * kLog2e;
   const bool drop = a.maskA != nullptr;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
-  const uint32_t* mrow = drop ? a.maskA + ((size_t)bh * S + (qvalid ? q : 0)) * a.W : nullptr;
+  const uint32_t* mcol = drop ? a.maskA + (size_t)bh * a.W * S + (qvalid ? q : 0) : nullptr;
   const bf16* kbase = a.k + (size_t)b * S * a.ld + h * D;
   const bf16* vbase = a.v + (size_t)b * S * a.ld + h * D;
 
@@ -483,7 +486,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(BwdArgs a) {
         pacc = mfma32(*reinterpret_cast<const bf16x8*>(&V[(kb * 32 + r) * KP + 16 * c + 8 * hh]), of[c], pacc);
       }
       const int kw = (k0 >> 5) + kb;
-      const uint32_t mw = drop && kw < a.W ? mrow[kw] : 0u;
+      const uint32_t mw = drop && kw < a.W ? mcol[(size_t)kw * S] : 0u;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int key = k0 + kb * 32 + crow(i, hh);

@@ -334,8 +334,10 @@ static bool wave_shape(int h) {
 }
 DTD_EXPORT int dtd_ln_bwd_num_partials(int rows, int h) {
   if (wave_shape(h)) {
+    // up to 1024 blocks x 4 waves = 4 waves per SIMD on 256 CUs: the row loop is a serial chain
+    // of loads -> wave reductions -> stores, so occupancy is what hides HBM latency
     int blocks = (rows + 3) / 4;
-    return blocks < 256 ? blocks : 256;
+    return blocks < 1024 ? blocks : 1024;
   }
   return rows < 256 ? rows : 256;
 }

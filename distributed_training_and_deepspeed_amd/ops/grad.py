@@ -17,6 +17,8 @@ SURVEY.md D3).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 
@@ -112,13 +114,39 @@ def emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
     if s == 1:
         gemm_into(dst, dy.t(), x, acc)
     else:
-        part = torch.bmm(dy.view(s, T // s, o).transpose(1, 2), x.view(s, T // s, i))
-        tot = part.sum(0, dtype=torch.float32)
-        if acc:
-            dst.add_(tot)
-        else:
-            dst.copy_(tot)
+        a, b = dy.view(s, T // s, o).transpose(1, 2), x.view(s, T // s, i)
+        part = _bmm_partials(a, b)
+        splitk_reduce(part, dst, acc)
     grad_done(p)
+
+
+_F32_PARTIALS = [os.environ.get("DTD_WGRAD_F32_PARTIALS", "1") == "1"]
+
+
+def _bmm_partials(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Batched K-slice products, in fp32 when hipBLASLt offers the bf16->fp32 batched GEMM
+    (no bf16 rounding of the partial sums), else in the input dtype."""
+    if _F32_PARTIALS[0] and a.dtype != torch.float32:
+        try:
+            return torch.bmm(a, b, out_dtype=torch.float32)
+        except (RuntimeError, TypeError):
+            _F32_PARTIALS[0] = False
+    return torch.bmm(a, b)
+
+
+def splitk_reduce(part: torch.Tensor, dst: torch.Tensor, acc: bool) -> None:
+    """dst (+)= part.sum(0) in fp32, one fused pass on GPU (ops/csrc/reduce.hip)."""
+    if dst.is_cuda:
+        from . import _lib
+        assert part.is_contiguous() and dst.is_contiguous() and part[0].numel() == dst.numel()
+        _lib.call("dtd_splitk_reduce", part.data_ptr(), _lib.dt(part), part.shape[0], dst.numel(),
+                  dst.data_ptr(), _lib.dt(dst), int(acc), _lib.stream())
+        return
+    tot = part.sum(0, dtype=torch.float32)
+    if acc:
+        dst.add_(tot.view_as(dst))
+    else:
+        dst.copy_(tot.view_as(dst))
 
 
 def emit_grad(p: torch.Tensor, g: torch.Tensor) -> None:

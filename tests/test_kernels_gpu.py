@@ -157,3 +157,31 @@ def test_sqnorm_and_scale_cast():
     y = torch.empty(x.numel(), dtype=torch.float32, device=DEV)
     Fx.scale_cast_(x, y, 0.25)
     close(y, x.float() * 0.25, 1e-6)
+
+
+@pytest.mark.parametrize("pdt,ddt,acc", [(torch.float32, torch.bfloat16, False), (torch.float32, torch.bfloat16, True),
+                                         (torch.bfloat16, torch.float32, True), (torch.float32, torch.float32, False)])
+def test_splitk_reduce(pdt, ddt, acc):
+    from distributed_training_and_deepspeed_amd.ops.grad import splitk_reduce
+    torch.manual_seed(0)
+    part = torch.randn(4, 96, 40).to(pdt)
+    dst = torch.randn(96, 40).to(ddt)
+    ref = (dst.float() if acc else 0) + part.float().sum(0)
+    g = dst.to(DEV)
+    splitk_reduce(part.to(DEV), g, acc)
+    close(g, ref, 1e-2 if ddt == torch.bfloat16 else 1e-5)
+
+
+def test_split_k_wgrad_matches_fp32():
+    from distributed_training_and_deepspeed_amd.ops.grad import emit_wgrad, wgrad_splits
+    torch.manual_seed(0)
+    T, o, i = 16384, 768, 3072
+    assert wgrad_splits(T, o, i) > 1
+    w = torch.nn.Parameter(torch.zeros(o, i, dtype=torch.bfloat16, device=DEV))
+    dy = torch.randn(T, o, device=DEV).to(torch.bfloat16)
+    x = torch.randn(T, i, device=DEV).to(torch.bfloat16)
+    emit_wgrad(w, dy, x)
+    ref = dy.float().t() @ x.float()
+    close(w.grad, ref, 1e-2)
+    emit_wgrad(w, dy, x)               # second contribution accumulates
+    close(w.grad, 2 * ref, 1e-2)
