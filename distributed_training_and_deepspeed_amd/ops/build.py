@@ -1,6 +1,6 @@
 """In-tree build of the gfx950 HIP kernel library (``ops/_dtd_kernels.so``).
 
-Every ``ops/csrc/*.hip`` file is compiled with ``hipcc --offload-arch=gfx950`` into an object
+Every ``ops/csrc/*.hip`` and ``comm/csrc/*.hip`` file is compiled with ``hipcc --offload-arch=gfx950`` into an object
 and linked into one shared library that exports a plain C ABI (``extern "C" dtd_*``).
 Python binds it with ctypes (``ops/_lib.py``) after ``import torch`` so the library resolves
 ``libamdhip64.so.7`` to the HIP runtime torch already loaded (one HIP runtime per process).
@@ -20,6 +20,7 @@ from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
+SRC_DIRS = (CSRC, HERE.parent / "comm" / "csrc")   # kernels + the native xGMI collectives
 LIB_NAME = "_dtd_kernels.so"
 LIB_PATH = HERE / LIB_NAME
 OBJ_DIR = HERE / "build"
@@ -34,11 +35,11 @@ def _hipcc() -> str:
 
 
 def sources() -> list[Path]:
-    return sorted(CSRC.glob("*.hip"))
+    return sorted(p for d in SRC_DIRS for p in d.glob("*.hip"))
 
 
 def _headers() -> list[Path]:
-    return sorted(CSRC.glob("*.h"))
+    return sorted(p for d in SRC_DIRS for p in d.glob("*.h"))
 
 
 def needs_build() -> bool:

@@ -30,6 +30,9 @@
 // counter RNG (mask index ((b*H+h)*S + q)*S + key, regenerated in backward), arbitrary S
 // (bounds-masked), head_dim 64 or 128.  q/k/v/o are strided views (row stride `ld`) into the
 // fused [B*S, 3*H*D] projection output, so no transpose/copy kernels are needed.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "common.h"
 
 using namespace dtd;
@@ -91,46 +94,51 @@ struct FwdArgs {
 // stores are contiguous too.
 // Keep(bh, q, key) = counter-RNG decision for flat element ((bh*S + q)*S + key), identical to
 // ops/rng.py keep_mask (so the math reference reproduces the masks bit for bit).
-// grid: (ceil(S/32), ceil(S/64), B*H); block: 64 = 32 queries x 2 key-words.
-__global__ void __launch_bounds__(64) attn_mask_kernel(uint32_t* __restrict__ maskA, uint32_t* __restrict__ maskB, int S,
-                                                       int W, const uint64_t* rng, uint32_t sid, uint32_t thr) {
+// grid: (ceil(S/32), B*H); block: 256 = 4 waves; each wave covers 32 queries x 2 key-words per
+// iteration and strides over the key-word pairs (few, fat workgroups: the work per element is a
+// handful of VALU ops, so workgroup dispatch -- not math -- bounds a one-wave-per-tile grid).
+__global__ void __launch_bounds__(256) attn_mask_kernel(uint32_t* __restrict__ maskA, uint32_t* __restrict__ maskB,
+                                                        int S, int W, const uint64_t* rng, uint32_t sid, uint32_t thr) {
   DropoutRng g(rng, sid);
-  const int lane = threadIdx.x, bh = blockIdx.z;
+  const int lane = threadIdx.x & 63, bh = blockIdx.y;
   const int q = blockIdx.x * 32 + (lane & 31);
-  const int kw = blockIdx.y * 2 + (lane >> 5);
-  uint32_t word = 0;
-  if (q < S && kw < W) {
-    const uint64_t base = ((uint64_t)bh * S + (uint64_t)q) * (uint64_t)S + (uint64_t)kw * 32;
-    const int nk = min(32, S - kw * 32);
-    if ((base & 1) == 0) {
+  const uint64_t rowbase = ((uint64_t)bh * S + (uint64_t)(q < S ? q : 0)) * (uint64_t)S;
+  for (int kp = threadIdx.x >> 6; kp < (W + 1) / 2; kp += 4) {
+    const int kw = kp * 2 + (lane >> 5);
+    uint32_t word = 0;
+    if (q < S && kw < W) {
+      const uint64_t base = rowbase + (uint64_t)kw * 32;
+      const int nk = min(32, S - kw * 32);
+      if ((base & 1) == 0) {
 #pragma unroll 4
-      for (int j = 0; j < 32; j += 2) {
-        const uint32_t b = g.bits((base + j) >> 1);
-        word |= (uint32_t)((b & 0xffffu) >= thr) << j;
-        word |= (uint32_t)((b >> 16) >= thr) << (j + 1);
+        for (int j = 0; j < 32; j += 2) {
+          const uint32_t b = g.bits((base + j) >> 1);
+          word |= (uint32_t)((b & 0xffffu) >= thr) << j;
+          word |= (uint32_t)((b >> 16) >= thr) << (j + 1);
+        }
+      } else {
+        for (int j = 0; j < 32; ++j) {
+          const uint64_t e = base + j;
+          const uint32_t b = g.bits(e >> 1);
+          const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
+          word |= (uint32_t)(h16 >= thr) << j;
+        }
       }
-    } else {
-      for (int j = 0; j < 32; ++j) {
-        const uint64_t e = base + j;
-        const uint32_t b = g.bits(e >> 1);
-        const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
-        word |= (uint32_t)(h16 >= thr) << j;
-      }
+      if (nk < 32) word &= (nk > 0 ? (0xffffffffu >> (32 - nk)) : 0u);
+      maskA[((size_t)bh * W + kw) * S + q] = word;
     }
-    if (nk < 32) word &= (nk > 0 ? (0xffffffffu >> (32 - nk)) : 0u);
-    maskA[((size_t)bh * W + kw) * S + q] = word;
-  }
-  // transpose through ballots: ballot j holds, for key-words kw0 (low half) and kw0+1 (high
-  // half), the q-bits of key 32*kw + j.  Lane j keeps the low word, lane 32+j the high word, so
-  // the 64 B-words leave in ONE store instruction.
-  uint32_t mine = 0;
+    // transpose through ballots: ballot j holds, for key-words kw0 (low half) and kw0+1 (high
+    // half), the q-bits of key 32*kw + j.  Lane j keeps the low word, lane 32+j the high word, so
+    // the 64 B-words leave in ONE store instruction.
+    uint32_t mine = 0;
 #pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const unsigned long long bal = __ballot((word >> j) & 1u);
-    if ((lane & 31) == j) mine = (lane < 32) ? (uint32_t)bal : (uint32_t)(bal >> 32);
+    for (int j = 0; j < 32; ++j) {
+      const unsigned long long bal = __ballot((word >> j) & 1u);
+      if ((lane & 31) == j) mine = (lane < 32) ? (uint32_t)bal : (uint32_t)(bal >> 32);
+    }
+    const int key = kp * 64 + lane;  // lane < 32: key-word kw0, lane >= 32: kw0 + 1
+    if (key < S) maskB[((size_t)bh * W + blockIdx.x) * S + key] = mine;
   }
-  const int key = blockIdx.y * 64 + lane;  // lane < 32: key-word kw0, lane >= 32: kw0 + 1
-  if (key < S) maskB[((size_t)bh * W + blockIdx.x) * S + key] = mine;
 }
 
 // Stage a [rows x D] bf16 tile (row stride `ld` in global) into registers, then LDS.
@@ -160,8 +168,8 @@ struct TileLoader {
 // grid: (ceil(S/128), B*H); block 256 = 4 waves x 32 queries.  KV tiles of 64 keys,
 // double-buffered in LDS with the next tile's global loads issued before the current tile's
 // MFMAs (written to the other buffer afterwards): one barrier per tile.
-template <int D>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(FwdArgs a) {
+template <int D, int OCC>
+__global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   constexpr int BN = 64, KP = D + 8, VP = D + 8, NC = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * VP];
@@ -309,8 +317,8 @@ struct BwdArgs {
 
 // dK, dV: grid (ceil(S/128), B*H); block 256 = 4 waves x 32 keys ("key on the lane").
 // Query tiles of 64 rows (Q, dO row-major in LDS, double-buffered).
-template <int D>
-__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(BwdArgs a) {
+template <int D, int OCC>
+__global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   constexpr int BM = 64, QP = D + 8, NC = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * QP];
   __shared__ __attribute__((aligned(16))) bf16 Os[2][BM * QP];
@@ -427,8 +435,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(BwdArgs a) {
 // dQ: grid (ceil(S/128), B*H); block 256 = 4 waves x 32 queries (query on the lane, as in the
 // forward); recomputes S^T and dP^T per 64-key tile and accumulates dQ^T = K^T.dS^T in
 // registers -- no atomics, no cross-workgroup reduction.
-template <int D>
-__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(BwdArgs a) {
+template <int D, int OCC>
+__global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   constexpr int BN = 64, KP = D + 8, NC = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * KP];
@@ -522,6 +530,18 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(BwdArgs a) {
 
 }  // namespace
 
+// Waves per SIMD the head_dim-64 kernels are compiled for (register budget 512/OCC per lane):
+// fwd, dK/dV, dQ.  Defaults are the measured best on MI355X (scripts/bench_attn.py); override
+// with DTD_ATTN_OCC="f,kv,q" for tuning runs.
+static int occupancy(int which) {
+  static const int defaults[3] = {2, 2, 2};
+  const char* env = getenv("DTD_ATTN_OCC");
+  if (!env) return defaults[which];
+  int v[3] = {defaults[0], defaults[1], defaults[2]};
+  sscanf(env, "%d,%d,%d", &v[0], &v[1], &v[2]);
+  return v[which];
+}
+
 // q,k,v,o: bf16 views with row stride ld (q/k/v) / ldo (o); lse: [B,H,S] fp32.
 // masks: [2][B*H*S*W] uint32 (W = ceil(S/32)) written here when p > 0 (read by the backward).
 DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const float* slopes,
@@ -534,15 +554,22 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
     if (!masks) return (int)hipErrorInvalidValue;
     mA = masks;
     uint32_t* mB = masks + (size_t)B * H * S * W;
-    hipLaunchKernelGGL(attn_mask_kernel, dim3(W, (S + 63) / 64, B * H), dim3(64), 0, s, mA, mB, S, W, rng, sid,
+    hipLaunchKernelGGL(attn_mask_kernel, dim3(W, B * H), dim3(256), 0, s, mA, mB, S, W, rng, sid,
                        keep_threshold(p));
   }
   FwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, slopes, mA, B, S, H, ld, ldo, causal, W,
             scale, p};
   dim3 grid((S + 127) / 128, B * H);
-  if (D == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, a);
-  else if (D == 128) hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, s, a);
-  else return (int)hipErrorInvalidValue;
+  if (D == 64) {
+    const int o = occupancy(0);
+    if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3>), grid, dim3(256), 0, s, a);
+    else if (o == 2) hipLaunchKernelGGL((attn_fwd_kernel<64, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(256), 0, s, a);
+  } else if (D == 128) {
+    hipLaunchKernelGGL((attn_fwd_kernel<128, 1>), grid, dim3(256), 0, s, a);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
   DTD_LAUNCH_CHECK();
 }
 
@@ -562,12 +589,16 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
             (bf16*)dv, slopes, mA, mB, B, S, H, ld, ldo, causal, W, scale, p};
   if (D == 64) {
     hipLaunchKernelGGL(attn_bwd_delta_kernel<64>, dim3(B * S), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<64>, grid, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, grid, dim3(256), 0, s, a);
+    if (occupancy(1) >= 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 1>), grid, dim3(256), 0, s, a);
+    const int o = occupancy(2);
+    if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3>), grid, dim3(256), 0, s, a);
+    else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1>), grid, dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL(attn_bwd_delta_kernel<128>, dim3(B * S), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<128>, grid, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<128>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<128, 1>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<128, 1>), grid, dim3(256), 0, s, a);
   }
   DTD_LAUNCH_CHECK();
 }

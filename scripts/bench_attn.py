@@ -1,0 +1,46 @@
+#!/usr/bin/env python
+"""Time the flash-attention kernels at the BERT-base training shape for several occupancy
+variants (DTD_ATTN_OCC="fwd,dkdv,dq" waves/SIMD).  Prints one JSON line per variant."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_training_and_deepspeed_amd.ops import attention as A  # noqa: E402
+from distributed_training_and_deepspeed_amd.ops.rng import RngState  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def main():
+    B, S, H, D = int(os.environ.get("B", 32)), 512, 12, 64
+    p = float(os.environ.get("P", 0.1))
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda").to(torch.bfloat16)
+    dctx = torch.randn(B * S, H * D, device="cuda").to(torch.bfloat16)
+    rng = RngState(1, device="cuda")
+    flops_f = 4 * B * H * S * S * D
+    for occ in sys.argv[1:] or ["1,1,1", "2,2,2", "3,2,2", "3,2,3"]:
+        os.environ["DTD_ATTN_OCC"] = occ
+        ctx, lse, mk = A.attn_fwd(qkv, B, S, H, D, False, None, p, rng, 3)
+        tf = timeit(lambda: A.attn_fwd(qkv, B, S, H, D, False, None, p, rng, 3))
+        tb = timeit(lambda: A.attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, False, None, p, rng, 3, mk))
+        print(json.dumps({"occ": occ, "B": B, "p": p, "fwd_us": round(tf, 1), "bwd_us": round(tb, 1),
+                          "fwd_TFs": round(flops_f / tf / 1e6, 1), "bwd_TFs": round(2.5 * flops_f / tb / 1e6, 1)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
