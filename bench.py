@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--grad-dtype", default=None, choices=[None, "bf16", "fp32"])
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("DTD_BUCKET_MB", "64")))
     ap.add_argument("--impl", default="fused", choices=["fused", "reference"])
+    ap.add_argument("--small-bucket-allreduce", default="rccl", choices=["rccl", "xgmi"],
+                    help="xgmi: buckets <= 4 MiB use the native peer-mapped all-reduce kernel")
     ap.add_argument("--dense-mlm-head", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
@@ -77,7 +79,8 @@ def main():
         model.rt.exact_dropout = False  # torch-eager baseline: ATen dropout, HF-style eager ops
     model.train()
     gdt = {"bf16": torch.bfloat16, "fp32": torch.float32}.get(args.grad_dtype, dtype)
-    ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt,
+                                  small_bucket_allreduce=args.small_bucket_allreduce)
     opt = hf_adamw(ddp.parameters(), lr=5e-5)
 
     B, S = args.batch_size, args.seq_len

@@ -169,12 +169,15 @@ class _FusedLayerFn(torch.autograd.Function):
         sa, s1, s2 = rng.sid(layer.sid_attn), rng.sid(layer.sid_1), rng.sid(layer.sid_2)
         x2d = x.reshape(T, h)
         eps = c.ln_eps
+        # attention-dropout keep bits: generated on a side stream, overlapping the QKV GEMM
+        pend = A.attn_masks_async(B, S, H, D, p_a, rng, sa, x.device) \
+            if x.is_cuda and x.dtype == torch.bfloat16 else None
         if c.pre_ln:
             _, a_in, m1, r1 = Fx.ln_fwd(None, x2d, g1, b1, eps, 0.0, rng, 0)
         else:
             a_in = x2d
         qkv = F.linear(a_in, qkv_w, qkv_b)
-        actx, lse, amask = A.attn_fwd(qkv, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa)
+        actx, lse, amask = A.attn_fwd(qkv, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, masks=pend)
         o = F.linear(actx, o_w, o_b)
         if c.pre_ln:
             z1, f_in, m2, r2 = Fx.ln_fwd(o, x2d, g2, b2, eps, p_h, rng, s1)

@@ -55,6 +55,7 @@ _SIGS = {
     # attention.hip
     "dtd_attn_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, U32, P]),
     "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
+    "dtd_attn_masks": (I, [P, I, I, I, F, P, U32, P]),
     # reduce.hip
     "dtd_splitk_reduce": (I, [P, I, I, ctypes.c_longlong, P, I, I, P]),
 }

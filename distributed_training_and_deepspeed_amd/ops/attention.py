@@ -107,9 +107,49 @@ def kernel_supported(qkv: torch.Tensor, D: int) -> bool:
     return qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128) and _lib.has("dtd_attn_fwd")
 
 
-def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | None = None, sid=0):
+_SIDE = {}
+
+
+def _side_stream(device) -> torch.cuda.Stream:
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device)
+    return s
+
+
+class PendingMasks:
+    """Dropout keep-bit masks being generated on a side stream (see ``attn_masks_async``)."""
+
+    def __init__(self, masks: torch.Tensor, event: torch.cuda.Event):
+        self.masks, self.event = masks, event
+
+
+def attn_masks_async(B, S, H, D, p, rng: RngState, sid, device) -> PendingMasks | None:
+    """Start generating the attention-dropout keep bits on a side stream.  The kernel is pure
+    VALU (counter-RNG hashing) and independent of the activations, so issued before the QKV
+    projection it runs concurrently with that MFMA-bound GEMM; ``attn_fwd(masks=...)`` joins
+    it.  Returns None when the kernel path is not used (CPU / reference)."""
+    if p <= 0 or not torch.cuda.is_available() or torch.device(device).type != "cuda" or D not in (64, 128) \
+            or not _lib.has("dtd_attn_masks"):
+        return None
+    cur = torch.cuda.current_stream(device)
+    W = (S + 31) // 32
+    masks = torch.empty((2, B * H * S * W), dtype=torch.int32, device=device)
+    side = _side_stream(torch.device(device))
+    side.wait_stream(cur)                      # the rng step / previous users of the buffer
+    with torch.cuda.stream(side):
+        _lib.call("dtd_attn_masks", masks.data_ptr(), B, S, H, float(p), rng.state.data_ptr(), sid,
+                  side.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    return PendingMasks(masks, ev)
+
+
+def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | None = None, sid=0,
+             masks: PendingMasks | None = None):
     """Returns (ctx [B*S, H*D], lse [B, H, S] fp32, masks).  ``masks`` holds the dropout keep
-    bits for the backward ([2, B*H*S*ceil(S/32)] int32 on the kernel path, None otherwise)."""
+    bits for the backward ([2, B*H*S*ceil(S/32)] int32 on the kernel path, None otherwise);
+    pass the ``attn_masks_async`` result to reuse masks generated ahead on a side stream."""
     if not kernel_supported(qkv, D):
         if qkv.is_cuda and qkv.dtype == torch.bfloat16 and _lib.has("dtd_attn_fwd") is False:
             _warn_once()
@@ -118,10 +158,15 @@ def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | 
     qkv = qkv.contiguous()
     ctx = torch.empty((B * S, H * D), dtype=qkv.dtype, device=qkv.device)
     lse = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
-    masks = None
-    if p > 0:
+    rng_ptr = rng.state.data_ptr() if rng is not None else None
+    if p > 0 and masks is not None:
+        torch.cuda.current_stream(qkv.device).wait_event(masks.event)
+        masks, rng_ptr = masks.masks, None     # generated already
+    elif p > 0:
         W = (S + 31) // 32
         masks = torch.empty((2, B * H * S * W), dtype=torch.int32, device=qkv.device)
+    else:
+        masks = None
     sl = slopes.to(device=qkv.device, dtype=torch.float32).contiguous() if slopes is not None else None
     # q/k/v are strided views into qkv: row stride 3*H*D, head stride D.
     ld = 3 * H * D
@@ -129,7 +174,7 @@ def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | 
     es = qkv.element_size()
     _lib.call("dtd_attn_fwd", base, base + H * D * es, base + 2 * H * D * es, ctx.data_ptr(), lse.data_ptr(),
               _lib.ptr(sl), _lib.ptr(masks), B, S, H, D, ld, H * D, int(causal), 1.0 / math.sqrt(D), float(p),
-              rng.state.data_ptr() if rng is not None else None, sid, _lib.stream())
+              rng_ptr, sid, _lib.stream())
     return ctx, lse, masks
 
 

@@ -534,7 +534,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
 // fwd, dK/dV, dQ.  Defaults are the measured best on MI355X (scripts/bench_attn.py); override
 // with DTD_ATTN_OCC="f,kv,q" for tuning runs.
 static int occupancy(int which) {
-  static const int defaults[3] = {2, 2, 2};
+  static const int defaults[3] = {3, 2, 3};
   const char* env = getenv("DTD_ATTN_OCC");
   if (!env) return defaults[which];
   int v[3] = {defaults[0], defaults[1], defaults[2]};
@@ -553,9 +553,13 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
   if (p > 0.f) {
     if (!masks) return (int)hipErrorInvalidValue;
     mA = masks;
-    uint32_t* mB = masks + (size_t)B * H * S * W;
-    hipLaunchKernelGGL(attn_mask_kernel, dim3(W, B * H), dim3(256), 0, s, mA, mB, S, W, rng, sid,
-                       keep_threshold(p));
+    // rng == nullptr: the masks were generated ahead of time by dtd_attn_masks (on a side
+    // stream, overlapping the QKV GEMM)
+    if (rng) {
+      uint32_t* mB = masks + (size_t)B * H * S * W;
+      hipLaunchKernelGGL(attn_mask_kernel, dim3(W, B * H), dim3(256), 0, s, mA, mB, S, W, rng, sid,
+                         keep_threshold(p));
+    }
   }
   FwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, slopes, mA, B, S, H, ld, ldo, causal, W,
             scale, p};
@@ -570,6 +574,18 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
   } else {
     return (int)hipErrorInvalidValue;
   }
+  DTD_LAUNCH_CHECK();
+}
+
+// Dropout keep-bit masks of one attention call ([2][B*H*S*W] uint32), VALU-only: launched on a
+// side stream so it runs concurrently with the (MFMA-bound) QKV projection GEMM.
+DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, const uint64_t* rng, uint32_t sid,
+                              hipStream_t s) {
+  if (B * S * H == 0 || p <= 0.f) return 0;
+  if (!masks || !rng) return (int)hipErrorInvalidValue;
+  const int W = (S + 31) / 32;
+  hipLaunchKernelGGL(attn_mask_kernel, dim3(W, B * H), dim3(256), 0, s, masks, masks + (size_t)B * H * S * W, S, W,
+                     rng, sid, keep_threshold(p));
   DTD_LAUNCH_CHECK();
 }
 

@@ -18,6 +18,9 @@ reducer:
   reference's fp32 buckets.  Bucket size defaults to the reference's 25 MiB; on an 8-GPU
   MI355X node larger buckets (fewer, bigger RCCL calls saturating the 7 xGMI links) are
   selected with ``bucket_cap_mb`` (see ``bench/`` sweep).
+* Optional native path for small buckets (``small_bucket_allreduce="xgmi"``): buckets of at
+  most ``xgmi_max_mb`` go through the peer-mapped one-shot/two-shot kernel of
+  ``comm/xgmi.py`` on a side stream instead of an RCCL ring (latency-bound sizes).
 * The constructor broadcasts parameters from rank 0 (C3).  Per-step buffer broadcast (C4) is
   elided: the only module buffers of the reference models are constant index tensors.
 """
@@ -43,10 +46,21 @@ class _Bucket:
         self.work = None
 
 
+class _StreamWork:
+    """Work handle of a collective issued on a side stream: wait() fences the current stream."""
+
+    def __init__(self, stream, device):
+        self.stream, self.device = stream, device
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, bucket_cap_mb: float = 25.0,
                  grad_dtype: torch.dtype | None = None, process_group=None, broadcast_parameters: bool = True,
-                 overlap: bool = True, flatten_params: bool = True):
+                 overlap: bool = True, flatten_params: bool = True, small_bucket_allreduce: str = "rccl",
+                 xgmi_max_mb: float = 4.0):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -65,6 +79,13 @@ class DistributedDataParallel(nn.Module):
         self._need_reset = True
         self._callback_queued = False
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
+        self._xgmi = None
+        if small_bucket_allreduce == "xgmi" and self.world > 1 and self.backend == "nccl":
+            from ..comm.xgmi import XgmiAllReduce
+            self._xgmi = XgmiAllReduce(process_group, max_bytes=int(xgmi_max_mb * 2 ** 20))
+            self._xgmi_stream = torch.cuda.Stream(self.device)
+        elif small_bucket_allreduce not in ("rccl", "xgmi"):
+            raise ValueError(f"small_bucket_allreduce must be 'rccl' or 'xgmi', got {small_bucket_allreduce!r}")
         if broadcast_parameters and self.world > 1:
             self._broadcast_params()
 
@@ -143,7 +164,13 @@ class DistributedDataParallel(nn.Module):
         if self.world == 1:
             return
         view = self.grads.buf[b.start:b.end]
-        if self.backend == "nccl":
+        if self._xgmi is not None and self._xgmi.supports(view):
+            side = self._xgmi_stream
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                self._xgmi.all_reduce(view, average=True)
+            b.work = _StreamWork(side, self.device)
+        elif self.backend == "nccl":
             b.work = comm_log.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
         else:
             b.work = comm_log.all_reduce(view, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
@@ -163,7 +190,7 @@ class DistributedDataParallel(nn.Module):
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
-                if self.backend != "nccl":
+                if self.backend != "nccl" and not isinstance(b.work, _StreamWork):
                     self.grads.buf[b.start:b.end].div_(self.world)
                 b.work = None
         self.grads.expose_as_grad()

@@ -49,3 +49,16 @@ def test_flash_attention_fwd_bwd(B, S, H, D, causal, alibi, p):
     for i, name in enumerate("qkv"):
         e = rel(g[:, :, i], r[:, :, i])
         assert e < 2e-2, f"d{name} rel err {e}"
+
+
+def test_side_stream_masks_match_inline_generation():
+    B, S, H, D, p = 2, 256, 4, 64, 0.1
+    torch.manual_seed(0)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda").to(torch.bfloat16)
+    rg = RngState(5, device="cuda")
+    c1, l1, m1 = A.attn_fwd(qkv, B, S, H, D, False, None, p, rg, 4)
+    pend = A.attn_masks_async(B, S, H, D, p, rg, 4, qkv.device)
+    assert pend is not None
+    c2, l2, m2 = A.attn_fwd(qkv, B, S, H, D, False, None, p, rg, 4, masks=pend)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m2) and torch.equal(c1, c2) and torch.equal(l1, l2)
