@@ -30,6 +30,7 @@ from distributed_training_and_deepspeed_amd.models import build_model, get_confi
 from distributed_training_and_deepspeed_amd.optim import hf_adamw  # noqa: E402
 from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel  # noqa: E402
 from distributed_training_and_deepspeed_amd.utils import get_device_count  # noqa: E402
+from distributed_training_and_deepspeed_amd.utils.tracing import StepTimer, enable_markers, marker  # noqa: E402
 
 
 def train(rank, world_size, batch_size, training_steps, bucket_size, model_name, opts):
@@ -57,16 +58,24 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
             progress = tqdm(range(training_steps))
         except ImportError:
             pass
+    if opts.markers:
+        enable_markers()
+    timer = StepTimer(batch_size * opts.seq_len, world_size)
     start = time.time()
     n = 0
     loss = None
     for batch in loader:
-        out = ddp(batch["input_ids"], labels=batch["labels"])
-        loss = out.loss
-        loss.backward()
-        optimizer.step()
-        optimizer.zero_grad()
-        model.rt.rng.advance()
+        timer.start()
+        with marker("forward"):
+            out = ddp(batch["input_ids"], labels=batch["labels"])
+            loss = out.loss
+        with marker("backward+allreduce"):
+            loss.backward()
+        with marker("optimizer"):
+            optimizer.step()
+            optimizer.zero_grad()
+            model.rt.rng.advance()
+        timer.stop()
         n += 1
         if progress is not None:
             progress.update(1)
@@ -78,6 +87,9 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
         tokens = n * batch_size * opts.seq_len * world_size
         print(json.dumps({"tokens_per_s": round(tokens / max(elapsed, 1e-9), 1), "steps_per_rank": n,
                           "world_size": world_size, "final_loss": round(float(loss.detach()), 4) if loss is not None else None}))
+        if opts.metrics_json:
+            timer.write(opts.metrics_json, {"model": name, "per_gpu_batch": batch_size, "seq_len": opts.seq_len,
+                                            "bucket_mb": bucket_size, "world_size": world_size})
     comm.destroy()
 
 
@@ -94,6 +106,8 @@ if __name__ == "__main__":
     parser.add_argument("--backend", default=None, choices=[None, "nccl", "gloo"])
     parser.add_argument("--impl", default="auto", choices=["auto", "fused", "reference"])
     parser.add_argument("--quiet", action="store_true")
+    parser.add_argument("--metrics-json", default="", help="write tokens/s, step-time percentiles, peak HBM here")
+    parser.add_argument("--markers", action="store_true", help="roctx ranges per phase (rocprofv3 --marker-trace)")
     args = parser.parse_args()
 
     device_count = args.device_count or get_device_count()

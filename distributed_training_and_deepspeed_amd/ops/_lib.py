@@ -98,10 +98,21 @@ def has(name: str) -> bool:
     return hasattr(lib(), name)
 
 
+DEBUG_SYNC = os.environ.get("DTD_DEBUG_SYNC", "0") == "1"
+
+
 def call(name: str, *args) -> None:
+    """Launch ``name``; raise on a launch error.  With ``DTD_DEBUG_SYNC=1`` (the framework's
+    HIP_LAUNCH_BLOCKING-style debug mode) every kernel is followed by a device
+    synchronisation, so an asynchronous fault is reported at the kernel that caused it."""
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise KernelError(f"{name} failed with hipError {rc}")
+    if DEBUG_SYNC:
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # noqa: PERF203
+            raise KernelError(f"{name}: device error after launch: {e}") from e
 
 
 def stream() -> int:

@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -413,6 +414,7 @@ class ZeroEngine(nn.Module):
         for s in self.units:
             if not s.launched:
                 self._reduce_unit(s)
+        self._release_pending()
         if self.comm_stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
 
@@ -476,6 +478,7 @@ class ZeroEngine(nn.Module):
     def _make_bwd_start(self, k: int):
         def hook(grad):
             s = self.units[k]
+            self._release_pending(keep=(s,))
             self._ensure(s)
             if s.gbuf is None:
                 self._alloc_landing(s)
@@ -485,10 +488,19 @@ class ZeroEngine(nn.Module):
         return hook
 
     def _reduce_unit(self, s: _Segment) -> None:
+        """Reduce-scatter a unit's gradients as soon as they are complete.  The gathered
+        parameters are released LATER (next unit's backward start / end of backward): the
+        backward that reported the last gradient may still read the weights for its dgrad."""
         if s.launched:
             return
         self._reduce_segment(s)
-        self._release(s)
+        s.pending_release = True
+
+    def _release_pending(self, keep=()) -> None:
+        for u in self.units:
+            if u.pending_release and u not in keep:
+                u.pending_release = False
+                self._release(u)
 
     # ================================================================== engine API
     def _reset(self) -> None:
@@ -553,6 +565,138 @@ class ZeroEngine(nn.Module):
 
     def zero_optimization_stage(self) -> int:
         return self.stage
+
+    # ================================================================== checkpointing
+    # DeepSpeed-compatible layout: <dir>/<tag>/mp_rank_00_model_states.pt holds the
+    # full module state (rank 0), <dir>/<tag>/zero_pp_rank_<r>_mp_rank_00_optim_states.pt holds rank
+    # r's flat shard (fp32 master, Adam moments, step), <dir>/latest names the newest tag.  Loading
+    # with the same world size / stage restores the shards exactly; otherwise the parameters are
+    # re-sharded from the full module state and the optimizer moments start fresh.
+    def _pid_names(self) -> dict:
+        names: dict = {}
+        for n, p in self.module.named_parameters(remove_duplicate=False):
+            names.setdefault(id(p), []).append(n)
+        return names
+
+    @torch.no_grad()
+    def full_state_dict(self) -> dict:
+        """Module state dict on CPU with every parameter materialised; stage 3 gathers one unit
+        at a time (collective: call on every rank)."""
+        names = self._pid_names()
+        sd = {}
+        in_units = set()
+        for s in self.units:
+            was = s.full is not None
+            self._ensure(s)
+            for p in s.params:
+                in_units.add(id(p))
+                t = p.detach().to("cpu", copy=True)
+                for n in names[id(p)]:
+                    sd[n] = t
+            if not was:
+                self._release(s)
+        for n, p in self.module.named_parameters(remove_duplicate=False):
+            if id(p) not in in_units:
+                sd[n] = p.detach().to("cpu", copy=True)
+        for n, b in self.module.named_buffers():
+            sd[n] = b.detach().to("cpu", copy=True)
+        return sd
+
+    def _ckpt_barrier(self):
+        if self.world > 1:
+            dist.barrier(group=self.group)
+
+    def _shard_file(self, path: str) -> str:
+        return os.path.join(path, f"zero_pp_rank_{self.shard_rank}_mp_rank_00_optim_states.pt")
+
+    @torch.no_grad()
+    def save_checkpoint(self, save_dir: str, tag=None, client_state: dict | None = None,
+                        save_latest: bool = True) -> str:
+        tag = str(tag) if tag is not None else f"global_step{self.global_steps}"
+        path = os.path.join(save_dir, tag)
+        if self.rank == 0:
+            os.makedirs(path, exist_ok=True)
+        self._ckpt_barrier()
+        if self.comm_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+        opt = self.optimizer
+        if self.stage > 0 or self.rank == 0:      # stage 0: the state is replicated
+            torch.save({"master": self.master.detach().cpu(), "exp_avg": opt.exp_avg.detach().cpu(),
+                        "exp_avg_sq": opt.exp_avg_sq.detach().cpu(), "step": opt.step_count,
+                        "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in opt.param_groups],
+                        "stage": self.stage, "world": self.world, "shard_numel": self.shard_numel,
+                        "global_steps": self.global_steps}, self._shard_file(path))
+        full = self.full_state_dict()
+        if self.rank == 0:
+            rt = getattr(self.module, "rt", None)
+            torch.save({"module": full, "global_steps": self.global_steps, "zero_stage": self.stage,
+                        "world_size": self.world, "client_state": client_state or {},
+                        "dropout_rng": rt.rng.state.detach().cpu() if rt is not None else None},
+                       os.path.join(path, "mp_rank_00_model_states.pt"))
+            if save_latest:
+                with open(os.path.join(save_dir, "latest"), "w") as f:
+                    f.write(tag)
+        self._ckpt_barrier()
+        return path
+
+    @torch.no_grad()
+    def load_checkpoint(self, load_dir: str, tag=None, load_optimizer_states: bool = True,
+                        load_module_only: bool = False):
+        """Returns (checkpoint path, client_state)."""
+        if tag is None:
+            with open(os.path.join(load_dir, "latest")) as f:
+                tag = f.read().strip()
+        path = os.path.join(load_dir, str(tag))
+        ms = torch.load(os.path.join(path, "mp_rank_00_model_states.pt"), map_location="cpu", weights_only=True)
+        shard_path = self._shard_file(path)
+        shard = None
+        if load_optimizer_states and not load_module_only and os.path.exists(shard_path):
+            shard = torch.load(shard_path, map_location="cpu", weights_only=True)
+            if (shard["stage"], shard["world"], shard["shard_numel"]) != (self.stage, self.world, self.shard_numel):
+                shard = None                       # different layout: re-shard from the module state
+        if shard is not None:
+            opt = self.optimizer
+            opt.load_state_dict({"step": shard["step"], "exp_avg": shard["exp_avg"], "exp_avg_sq": shard["exp_avg_sq"],
+                                 "master": shard["master"], "param_groups": shard["param_groups"]})
+            self._refresh_params()
+        else:
+            self._load_full(ms["module"])
+        self.global_steps = int(ms.get("global_steps", 0))
+        rt = getattr(self.module, "rt", None)
+        if rt is not None and ms.get("dropout_rng") is not None:   # dropout masks continue the same stream
+            rt.rng.state.copy_(ms["dropout_rng"])
+        self._need_reset = True
+        self._ckpt_barrier()
+        return path, ms.get("client_state", {})
+
+    @torch.no_grad()
+    def _load_full(self, sd: dict) -> None:
+        names = self._pid_names()
+        for s in self.buckets:
+            for p in s.params:
+                p.data.copy_(sd[names[id(p)][0]])
+            lo = self.shard_rank * s.chunk
+            self.master[s.shard_off:s.shard_off + s.chunk].copy_(s.full[lo:lo + s.chunk])
+            if self.lowp is not None and self.stage > 0:
+                self.lowp[s.shard_off:s.shard_off + s.chunk].copy_(s.full[lo:lo + s.chunk])
+        for s in self.units:
+            full = torch.zeros(s.numel, dtype=self.dtype, device=self.device)
+            for i, p in enumerate(s.params):
+                s.view(full, i).copy_(sd[names[id(p)][0]])
+            lo = self.rank * s.chunk
+            self.master[s.shard_off:s.shard_off + s.chunk].copy_(full[lo:lo + s.chunk])
+            if self.lowp is not None:
+                self.lowp[s.shard_off:s.shard_off + s.chunk].copy_(full[lo:lo + s.chunk])
+            if s.full is not None:
+                s.full.copy_(full)
+        for n, b in self.module.named_buffers():
+            if n in sd:
+                b.copy_(sd[n])
+        opt = self.optimizer
+        opt.exp_avg.zero_()
+        opt.exp_avg_sq.zero_()
+        opt.step_count = 0
+        opt.hp[5] = 0.0
 
     def train(self, mode: bool = True):
         self.module.train(mode)

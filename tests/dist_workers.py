@@ -79,3 +79,41 @@ def allreduce_worker(rank, world, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     t = mod.all_reduce_example(rank, world, "gloo")
     torch.save(t, os.path.join(out_dir, f"ar{rank}.pt"))
+
+
+def zero_ckpt_worker(rank, world, port, out_dir, stage, load_stage):
+    """Train 2 steps, checkpoint, train 2 more; a fresh engine (other init, maybe other stage)
+    loads the checkpoint and trains the same 2 steps."""
+    from distributed_training_and_deepspeed_amd.parallel.zero import initialize
+    comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
+
+    def engine(st, seed):
+        model = build_model("tiny", impl="fused", seed=seed)
+        cfg = {"optimizer": {"type": "Adam", "params": {"lr": 1e-3}},
+               "zero_optimization": {"stage": st, "reduce_bucket_size": 50000}}
+        return initialize(model=model, model_parameters=model.parameters(), config=cfg)[0]
+
+    ids, lab = _batches(build_model("tiny", seed=3).cfg, rank, world, 4)
+
+    def run(eng, steps):
+        for i in steps:
+            eng.backward(eng(ids[i], labels=lab[i]).loss)
+            eng.step()
+
+    a = engine(stage, 3)
+    run(a, range(2))
+    ck = os.path.join(out_dir, "ckpt")
+    a.save_checkpoint(ck, client_state={"epoch": 7})
+    saved = a.full_state_dict()
+    run(a, range(2, 4))
+    fa = a.full_state_dict()
+    b = engine(load_stage, 99)
+    path, client = b.load_checkpoint(ck)
+    gs = b.global_steps
+    loaded = b.full_state_dict()
+    run(b, range(2, 4))
+    fb = b.full_state_dict()
+    if rank == 0:
+        torch.save({"saved": saved, "loaded": loaded, "fa": fa, "fb": fb, "client": client, "tag": os.path.basename(path),
+                    "gs": gs}, os.path.join(out_dir, f"ck{stage}{load_stage}.pt"))
+    comm.destroy()

@@ -95,3 +95,15 @@ def test_pytorch_allreduce_demo(tmp_path, free_port):
     _spawn(W.allreduce_worker, 3, free_port, str(tmp_path))
     for r in range(3):
         assert torch.load(tmp_path / f"ar{r}.pt", weights_only=True).tolist() == [15, 27, 39]
+
+
+@pytest.mark.parametrize("stage,load_stage", [(1, 1), (2, 2), (3, 3), (3, 1), (0, 2)])
+def test_zero_checkpoint_roundtrip(tmp_path, free_port, stage, load_stage):
+    _spawn(W.zero_ckpt_worker, 2, free_port, str(tmp_path), stage, load_stage)
+    r = torch.load(tmp_path / f"ck{stage}{load_stage}.pt", weights_only=True)
+    assert r["client"] == {"epoch": 7} and r["tag"] == "global_step2" and r["gs"] == 2
+    for k in r["saved"]:
+        assert torch.equal(r["saved"][k], r["loaded"][k]), k      # parameters restored exactly
+    if stage == load_stage:                                         # shards + moments + rng restored:
+        for k in r["fa"]:                                           # training continues identically
+            assert torch.equal(r["fa"][k], r["fb"][k]), k
