@@ -222,11 +222,13 @@ class _FusedLayerFn(torch.autograd.Function):
                                 dgamma=_acc(g2), dbeta=_acc(b2), dbias=_acc(bf2))
             for p in (g2, b2, bf2):
                 grad_done(p)
-        a = Fx.act_fwd(u, c.activation)
-        emit_wgrad(w2, dy, a)
+        # dgrad first: the activation a = act(u) (fc2's wgrad input) is then recomputed inside the
+        # activation-backward pass instead of a separate act_fwd read/write of the T x 4h tensor
         da = dy @ w2
-        du = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1))
+        du, a = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1), want_act=True)
         grad_done(bf1)
+        emit_wgrad(w2, dy, a)
+        del a
         emit_wgrad(w1, du, f_in)
         if c.pre_ln:
             dfin = du @ w1

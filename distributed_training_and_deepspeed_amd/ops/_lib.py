@@ -35,7 +35,7 @@ _SIGS = {
     # act.hip
     "dtd_act_fwd": (I, [I, P, P, SZ, I, P]),
     "dtd_act_bwd_num_partials": (I, [I, I]),
-    "dtd_act_bwd": (I, [I, P, P, P, P, I, I, I, P]),
+    "dtd_act_bwd": (I, [I, P, P, P, P, P, I, I, I, P]),
     "dtd_colsum_finalize": (I, [P, I, I, P, I, I, F, P]),
     "dtd_colsum_finalize_multi": (I, [I, P, I, I, P, I, I, P, I, I, P, I, I, P]),
     "dtd_embed_word_bwd_chunked": (I, [I, I, P, P, P, P, P, P, P, I, I, I, I, P]),

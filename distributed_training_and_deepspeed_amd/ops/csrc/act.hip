@@ -59,14 +59,16 @@ __global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ u, T
   }
 }
 
-// du = dy * act'(u) (act == kNone: du = dy), plus per-block column partials of du.
+// du = dy * act'(u) (act == kNone: du = dy), plus per-block column partials of du.  With
+// `yout`, the activation act(u) is recomputed in the same pass (the FFN backward needs it for
+// the second projection's weight gradient; storing it in forward would cost a T x 4h tensor).
 // grid = (ceil(cols / (64*VEC)), G); block = 4 waves sharing one 64*VEC-column tile; each wave
 // strides over rows with 4 rows in flight (ILP), and the 4 waves' column sums are combined
 // through LDS into one partial row per block row-group.
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ u,
                                                       T* __restrict__ du, float* __restrict__ part,
-                                                      int rows, int cols, int act) {
+                                                      T* __restrict__ yout, int rows, int cols, int act) {
   __shared__ float sh[4][64 * VEC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = (blockIdx.x * 64 + lane) * VEC;
@@ -87,6 +89,12 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, 
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
+        if (yout) {
+          float a[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) a[j] = act_f(act, x[k][j]);
+          vstore<T, VEC>(yout + (size_t)(r + k * stride) * cols + col, a);
+        }
         if (act != kNone) {
 #pragma unroll
           for (int j = 0; j < VEC; ++j) d[k][j] *= act_df(act, x[k][j]);
@@ -103,6 +111,12 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, 
       if (act != kNone) {
         float x[VEC];
         vload<T, VEC>(u + off, x);
+        if (yout) {
+          float a[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) a[j] = act_f(act, x[j]);
+          vstore<T, VEC>(yout + off, a);
+        }
 #pragma unroll
         for (int j = 0; j < VEC; ++j) d[j] *= act_df(act, x[j]);
       }
@@ -122,20 +136,20 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, 
 }
 
 template <typename T, int VEC>
-void launch_act_bwd(const void* dy, const void* u, void* du, float* part, int rows, int cols, int act, int groups,
-                    hipStream_t s) {
+void launch_act_bwd(const void* dy, const void* u, void* du, float* part, void* yout, int rows, int cols, int act,
+                    int groups, hipStream_t s) {
   dim3 grid((cols / VEC + 63) / 64, groups);
-  hipLaunchKernelGGL((act_bwd_kernel<T, VEC>), grid, dim3(256), 0, s, (const T*)dy, (const T*)u, (T*)du, part, rows,
-                     cols, act);
+  hipLaunchKernelGGL((act_bwd_kernel<T, VEC>), grid, dim3(256), 0, s, (const T*)dy, (const T*)u, (T*)du, part,
+                     (T*)yout, rows, cols, act);
 }
 
 template <typename T>
-void dispatch_act_bwd(const void* dy, const void* u, void* du, float* part, int rows, int cols, int act, int groups,
-                      hipStream_t s) {
-  if (cols % 8 == 0) launch_act_bwd<T, 8>(dy, u, du, part, rows, cols, act, groups, s);
-  else if (cols % 4 == 0) launch_act_bwd<T, 4>(dy, u, du, part, rows, cols, act, groups, s);
-  else if (cols % 2 == 0) launch_act_bwd<T, 2>(dy, u, du, part, rows, cols, act, groups, s);
-  else launch_act_bwd<T, 1>(dy, u, du, part, rows, cols, act, groups, s);
+void dispatch_act_bwd(const void* dy, const void* u, void* du, float* part, void* yout, int rows, int cols, int act,
+                      int groups, hipStream_t s) {
+  if (cols % 8 == 0) launch_act_bwd<T, 8>(dy, u, du, part, yout, rows, cols, act, groups, s);
+  else if (cols % 4 == 0) launch_act_bwd<T, 4>(dy, u, du, part, yout, rows, cols, act, groups, s);
+  else if (cols % 2 == 0) launch_act_bwd<T, 2>(dy, u, du, part, yout, rows, cols, act, groups, s);
+  else launch_act_bwd<T, 1>(dy, u, du, part, yout, rows, cols, act, groups, s);
 }
 
 // out[c] = (accumulate ? out[c] : 0) + scale * sum_p part[p][c]; fixed summation order.
@@ -145,27 +159,31 @@ struct FinalizeSet {
   const float* part[4]; void* out[4]; int dtype[4]; int acc[4];
 };
 
+// Column sums of [nparts x cols] fp32 partials.  Block = 16 columns x 64 row-lanes (1024
+// threads): each wave reads 4 rows x 16 columns (64 B segments), so a 768-wide array spreads
+// over 48 blocks per partial array instead of 12 (the finalize is latency-, not bandwidth-bound).
+// Fixed summation order: deterministic.
 __global__ void __launch_bounds__(1024) colsum_finalize_kernel(FinalizeSet fs, int nparts, int cols, float scale) {
-  __shared__ float sh[16][65];
-  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lane;
+  __shared__ float sh[64][17];
+  const int c = threadIdx.x & 15, rl = threadIdx.x >> 4;  // rl: row-lane 0..63
+  const int col = blockIdx.x * 16 + c;
   const int k = blockIdx.y;
   const float* part = fs.part[k];
   float t0 = 0.f, t1 = 0.f;
   if (col < cols) {
-    int p = sl;
-    for (; p + 16 < nparts; p += 32) {
+    int p = rl;
+    for (; p + 64 < nparts; p += 128) {
       t0 += part[(size_t)p * cols + col];
-      t1 += part[(size_t)(p + 16) * cols + col];
+      t1 += part[(size_t)(p + 64) * cols + col];
     }
     if (p < nparts) t0 += part[(size_t)p * cols + col];
   }
-  sh[sl][lane] = t0 + t1;
+  sh[rl][c] = t0 + t1;
   __syncthreads();
-  if (sl == 0 && col < cols) {
+  if (rl == 0 && col < cols) {
     float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s += sh[i][lane];
+#pragma unroll 16
+    for (int i = 0; i < 64; ++i) s += sh[i][c];
     s *= scale;
     if (fs.dtype[k] == kBF16) {
       bf16* o = (bf16*)fs.out[k];
@@ -200,12 +218,14 @@ DTD_EXPORT int dtd_act_bwd_num_partials(int rows, int cols) {
   return g;
 }
 
-DTD_EXPORT int dtd_act_bwd(int dtype, const void* dy, const void* u, void* du, float* part, int rows, int cols,
-                           int act, hipStream_t s) {
+// yout (may be null): also write act(u) -- requires act != none.
+DTD_EXPORT int dtd_act_bwd(int dtype, const void* dy, const void* u, void* du, float* part, void* yout, int rows,
+                           int cols, int act, hipStream_t s) {
   if (rows <= 0) return 0;
+  if (yout && (act == kNone || !u)) return (int)hipErrorInvalidValue;
   const int groups = dtd_act_bwd_num_partials(rows, cols);
-  if (dtype == kBF16) dispatch_act_bwd<bf16>(dy, u, du, part, rows, cols, act, groups, s);
-  else dispatch_act_bwd<float>(dy, u, du, part, rows, cols, act, groups, s);
+  if (dtype == kBF16) dispatch_act_bwd<bf16>(dy, u, du, part, yout, rows, cols, act, groups, s);
+  else dispatch_act_bwd<float>(dy, u, du, part, yout, rows, cols, act, groups, s);
   DTD_LAUNCH_CHECK();
 }
 
@@ -214,7 +234,7 @@ DTD_EXPORT int dtd_colsum_finalize(const float* part, int nparts, int cols, void
   if (cols <= 0) return 0;
   FinalizeSet fs{};
   fs.part[0] = part; fs.out[0] = out; fs.dtype[0] = out_dtype; fs.acc[0] = accumulate;
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 63) / 64, 1), dim3(1024), 0, s, fs, nparts, cols, scale);
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 15) / 16, 1), dim3(1024), 0, s, fs, nparts, cols, scale);
   DTD_LAUNCH_CHECK();
 }
 
@@ -229,6 +249,6 @@ DTD_EXPORT int dtd_colsum_finalize_multi(int n, const float* parts, int nparts, 
     fs.part[i] = parts + (size_t)i * nparts * cols;
     fs.out[i] = outs[i]; fs.dtype[i] = dts[i]; fs.acc[i] = accs[i];
   }
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 63) / 64, n), dim3(1024), 0, s, fs, nparts, cols, 1.f);
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 15) / 16, n), dim3(1024), 0, s, fs, nparts, cols, 1.f);
   DTD_LAUNCH_CHECK();
 }

@@ -41,12 +41,23 @@ __device__ __forceinline__ float drop_factor(const DropoutRng& g, uint64_t e, ui
   return h16 >= thr ? scale : 0.f;
 }
 
-template <typename T, int VEC, int ITERS>
+// Sum over the LPR lanes of a row group (LPR = 64: whole wave; 32: half-wave rows).
+template <int LPR>
+__device__ __forceinline__ float row_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// LPR lanes per row (64, or 32 = two rows per wave so that h = 768 / 1280 rows still move in
+// 16-byte bf16x8 vectors: 768 = 32 lanes x 3 x 8).
+template <typename T, int VEC, int ITERS, int LPR>
 __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
-  constexpr int NPL = VEC * ITERS;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= a.rows) return;
+  constexpr int NPL = VEC * ITERS, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int row0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool valid = row0 < a.rows;
+  const int row = valid ? row0 : a.rows - 1;     // keep every lane of the wave in the shuffles
   const int h = a.h;
   const size_t base = (size_t)row * h;
   const bool has_drop = a.p > 0.f && a.y != nullptr;
@@ -56,7 +67,7 @@ __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
   float z[NPL];
 #pragma unroll
   for (int c = 0; c < ITERS; ++c) {
-    const int col = (c * 64 + lane) * VEC;
+    const int col = (c * LPR + sub) * VEC;
     float t[VEC];
     if (a.y) {
       vload<T, VEC>((const T*)a.y + base + col, t);
@@ -74,22 +85,23 @@ __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
 #pragma unroll
       for (int j = 0; j < VEC; ++j) t[j] += rr[j];
     }
-    if (a.z) vstore<T, VEC>((T*)a.z + base + col, t);
+    if (a.z && valid) vstore<T, VEC>((T*)a.z + base + col, t);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) z[c * VEC + j] = t[j];
   }
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NPL; ++i) s += z[i];
-  const float mu = wave_sum(s) / h;
+  const float mu = row_sum<LPR>(s) / h;
   float v = 0.f;
 #pragma unroll
   for (int i = 0; i < NPL; ++i) { float d = z[i] - mu; v += d * d; }
-  const float rs = rsqrtf(wave_sum(v) / h + a.eps);
-  if (lane == 0) { a.mean[row] = mu; a.rstd[row] = rs; }
+  const float rs = rsqrtf(row_sum<LPR>(v) / h + a.eps);
+  if (!valid) return;
+  if (sub == 0) { a.mean[row] = mu; a.rstd[row] = rs; }
 #pragma unroll
   for (int c = 0; c < ITERS; ++c) {
-    const int col = (c * 64 + lane) * VEC;
+    const int col = (c * LPR + sub) * VEC;
     float gm[VEC], bt[VEC], o[VEC];
     vload<T, VEC>((const T*)a.gamma + col, gm);
     vload<T, VEC>((const T*)a.beta + col, bt);
@@ -99,10 +111,10 @@ __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
   }
 }
 
-template <typename T, int VEC, int ITERS>
+template <typename T, int VEC, int ITERS, int LPR>
 __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
-  constexpr int NPL = VEC * ITERS;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  constexpr int NPL = VEC * ITERS, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6, sub = lane % LPR;
   const int h = a.h;
   const bool has_drop = a.p > 0.f && a.dy != nullptr;
   DropoutRng g(a.rng, a.stream_id);
@@ -112,16 +124,23 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
 #pragma unroll
   for (int i = 0; i < NPL; ++i) { pg[i] = 0.f; pb[i] = 0.f; py[i] = 0.f; }
 #pragma unroll
-  for (int c = 0; c < ITERS; ++c) vload<T, VEC>((const T*)a.gamma + (c * 64 + lane) * VEC, gm + c * VEC);
+  for (int c = 0; c < ITERS; ++c) vload<T, VEC>((const T*)a.gamma + (c * LPR + sub) * VEC, gm + c * VEC);
 
-  for (int row = blockIdx.x * nw + w; row < a.rows; row += gridDim.x * nw) {
+  // both half-waves of an LPR=32 wave run the same trip count (rows are padded by clamping and
+  // masked), so the row reductions' cross-lane shuffles always see a fully active wave
+  const int rstride = gridDim.x * nw * RPW;
+  for (int rb = (blockIdx.x * nw + w) * RPW; rb < a.rows; rb += rstride) {
+    const int row0 = rb + lane / LPR;
+    const bool valid = row0 < a.rows;
+    const int row = valid ? row0 : a.rows - 1;
     const size_t base = (size_t)row * h;
     const float mu = a.mean[row], rs = a.rstd[row];
     float xh[NPL], dg[NPL];
     float s1 = 0.f, s2 = 0.f;
+    const float vm = valid ? 1.f : 0.f;   // padded rows contribute nothing to the partials
 #pragma unroll
     for (int c = 0; c < ITERS; ++c) {
-      const int col = (c * 64 + lane) * VEC;
+      const int col = (c * LPR + sub) * VEC;
       float zz[VEC], dd[VEC];
       vload<T, VEC>((const T*)a.z + base + col, zz);
       vload<T, VEC>((const T*)a.dout + base + col, dd);
@@ -132,14 +151,15 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
         dg[i] = dd[j] * gm[i];
         s1 += dg[i];
         s2 += dg[i] * xh[i];
-        pg[i] += dd[j] * xh[i];
-        pb[i] += dd[j];
+        pg[i] += vm * dd[j] * xh[i];
+        pb[i] += vm * dd[j];
       }
     }
-    const float m1 = wave_sum(s1) / h, m2 = wave_sum(s2) / h;
+    const float m1 = row_sum<LPR>(s1) / h, m2 = row_sum<LPR>(s2) / h;
+    if (!valid) continue;
 #pragma unroll
     for (int c = 0; c < ITERS; ++c) {
-      const int col = (c * 64 + lane) * VEC;
+      const int col = (c * LPR + sub) * VEC;
       float dz[VEC];
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
@@ -164,6 +184,14 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
       }
     }
   }
+  if constexpr (LPR < 64) {   // fold the half-waves (same columns, different rows)
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      pg[i] += __shfl_xor(pg[i], 32, 64);
+      pb[i] += __shfl_xor(pb[i], 32, 64);
+      py[i] += __shfl_xor(py[i], 32, 64);
+    }
+  }
   // Block-level reduction of the column partials through LDS (one array at a time).
   __shared__ float sh[4][2048];  // nw <= 4 waves, h <= 2048
   float* outs[3] = {a.part_gamma, a.part_beta, a.part_bias};
@@ -175,7 +203,7 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
 #pragma unroll
     for (int c = 0; c < ITERS; ++c)
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) sh[w][(c * 64 + lane) * VEC + j] = srcs[k][c * VEC + j];
+      for (int j = 0; j < VEC; ++j) sh[w][(c * LPR + sub) * VEC + j] = srcs[k][c * VEC + j];
     __syncthreads();
     for (int col = threadIdx.x; col < h; col += blockDim.x) {
       float t = 0.f;
@@ -298,30 +326,30 @@ __global__ void __launch_bounds__(256) ln_bwd_block(LnBwdArgs a) {
   }
 }
 
-template <typename T, int VEC, int ITERS>
+template <typename T, int VEC, int ITERS, int LPR = 64>
 bool try_wave(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream_t s) {
   const int h = f ? f->h : b->h;
-  if (h != 64 * VEC * ITERS) return false;
+  if (h != LPR * VEC * ITERS) return false;
   if (f) {
-    const int rows_per_block = 4;
-    hipLaunchKernelGGL((ln_fwd_wave<T, VEC, ITERS>), dim3((f->rows + rows_per_block - 1) / rows_per_block),
+    const int rows_per_block = 4 * (64 / LPR);
+    hipLaunchKernelGGL((ln_fwd_wave<T, VEC, ITERS, LPR>), dim3((f->rows + rows_per_block - 1) / rows_per_block),
                        dim3(256), 0, s, *f);
   } else {
-    hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS>), dim3(nblocks_bwd), dim3(256), 0, s, *b);
+    hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, LPR>), dim3(nblocks_bwd), dim3(256), 0, s, *b);
   }
   return true;
 }
 
 template <typename T>
 void dispatch(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream_t s) {
-  if (try_wave<T, 2, 1>(f, b, nblocks_bwd, s)) return;     // h = 128
-  if (try_wave<T, 4, 1>(f, b, nblocks_bwd, s)) return;     // 256
-  if (try_wave<T, 8, 1>(f, b, nblocks_bwd, s)) return;     // 512
-  if (try_wave<T, 4, 3>(f, b, nblocks_bwd, s)) return;     // 768
-  if (try_wave<T, 8, 2>(f, b, nblocks_bwd, s)) return;     // 1024
-  if (try_wave<T, 4, 5>(f, b, nblocks_bwd, s)) return;     // 1280
-  if (try_wave<T, 8, 3>(f, b, nblocks_bwd, s)) return;     // 1536
-  if (try_wave<T, 8, 4>(f, b, nblocks_bwd, s)) return;     // 2048
+  if (try_wave<T, 2, 1>(f, b, nblocks_bwd, s)) return;      // h = 128
+  if (try_wave<T, 4, 1>(f, b, nblocks_bwd, s)) return;      // 256
+  if (try_wave<T, 8, 1>(f, b, nblocks_bwd, s)) return;      // 512
+  if (try_wave<T, 8, 3, 32>(f, b, nblocks_bwd, s)) return;  // 768: two rows per wave, 16 B/lane
+  if (try_wave<T, 8, 2>(f, b, nblocks_bwd, s)) return;      // 1024
+  if (try_wave<T, 8, 5, 32>(f, b, nblocks_bwd, s)) return;  // 1280: two rows per wave
+  if (try_wave<T, 8, 3>(f, b, nblocks_bwd, s)) return;      // 1536
+  if (try_wave<T, 8, 4>(f, b, nblocks_bwd, s)) return;      // 2048
   if (f) hipLaunchKernelGGL((ln_fwd_block<T>), dim3(f->rows), dim3(256), 0, s, *f);
   else hipLaunchKernelGGL((ln_bwd_block<T>), dim3(nblocks_bwd), dim3(256), 0, s, *b);
 }

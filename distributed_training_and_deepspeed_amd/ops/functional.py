@@ -199,24 +199,30 @@ def act_fwd(u: torch.Tensor, act: str) -> torch.Tensor:
 
 
 def act_bwd(dy: torch.Tensor, u: torch.Tensor | None, act: str, dbias=None, acc: bool = False,
-            want_du: bool = True):
+            want_du: bool = True, want_act: bool = False):
     """du = dy * act'(u); writes column sums of du into ``dbias``.  act='none' is a plain
-    bias-gradient column sum of dy (returns dy)."""
+    bias-gradient column sum of dy (returns dy).  ``want_act``: also return act(u), recomputed
+    in the same pass -> (du, a)."""
     cols = dy.shape[-1]
     rows = dy.numel() // cols
+    if want_act and act == "none":
+        raise ValueError("want_act needs an activation")
     if not _on_gpu(dy):
         du = dy.float() if act == "none" else dy.float() * _ref_act_grad(u, act)
         _write_grad(dbias, du.view(rows, cols).sum(0), acc)
-        return du.to(dy.dtype) if want_du else None
+        du = du.to(dy.dtype) if want_du else None
+        return (du, act_fwd(u, act)) if want_act else du
     dy = dy.contiguous()
     du = torch.empty_like(dy) if (want_du and act != "none") else None
+    a = torch.empty_like(u) if want_act else None
     n = _lib.lib().dtd_act_bwd_num_partials(rows, cols)
     part = torch.empty((n, cols), dtype=torch.float32, device=dy.device) if dbias is not None else None
-    _lib.call("dtd_act_bwd", _lib.dt(dy), dy.data_ptr(), _lib.ptr(u), _lib.ptr(du), _lib.ptr(part), rows, cols,
-              ACT_CODES[act], _lib.stream())
+    _lib.call("dtd_act_bwd", _lib.dt(dy), dy.data_ptr(), _lib.ptr(u), _lib.ptr(du), _lib.ptr(part), _lib.ptr(a),
+              rows, cols, ACT_CODES[act], _lib.stream())
     if part is not None:
         _finalize(part, n, cols, dbias, acc)
-    return dy if act == "none" else du
+    du = dy if act == "none" else du
+    return (du, a) if want_act else du
 
 
 def bias_grad(dy: torch.Tensor, dbias: torch.Tensor, acc: bool = False) -> None:

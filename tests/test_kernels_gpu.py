@@ -46,11 +46,11 @@ def test_dropout_mask_matches_reference(dtype):
     assert abs(frac - 0.9) < 0.002
 
 
-@pytest.mark.parametrize("h", [128, 768, 1024, 384, 2304])
+@pytest.mark.parametrize("h", [128, 768, 1024, 1280, 384, 2304])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_layernorm_fwd_bwd(h, dtype):
     torch.manual_seed(0)
-    rows = 300
+    rows = 301  # odd: the two-rows-per-wave variants see a padded half-wave
     g, c = rng_pair()
     y = torch.randn(rows, h, dtype=dtype)
     r = torch.randn(rows, h, dtype=dtype)
@@ -82,9 +82,12 @@ def test_activation_fwd_bwd(act):
         a = Fx.act_fwd(u.to(dev), act)
         db = torch.zeros(3072, dtype=torch.float32, device=dev)
         du = Fx.act_bwd(dy.to(dev), u.to(dev), act, dbias=db)
-        res[dev] = (a, du, db)
+        db2 = torch.zeros(3072, dtype=torch.float32, device=dev)
+        du2, a2 = Fx.act_bwd(dy.to(dev), u.to(dev), act, dbias=db2, want_act=True)  # fused recompute
+        res[dev] = (a, du, db, a2, du2, db2)
     for a, b in zip(res[DEV], res["cpu"]):
         close(a, b, 2e-2)
+    assert torch.equal(res[DEV][0], res[DEV][3]) and torch.equal(res[DEV][1], res[DEV][4])
 
 
 @pytest.mark.parametrize("V", [28996, 50257, 1000, 250880])
