@@ -238,10 +238,11 @@ class _FusedLayerFn(torch.autograd.Function):
             for p in (g2, b2, o_b):
                 grad_done(p)
         else:
-            # f_in = LN1(z1) feeds both the FFN and (as residual) z2
-            dfin = torch.addmm(dz2, du, w1)
+            # f_in = LN1(z1) feeds both the FFN and (as residual) z2: d f_in = du.W1 + dz2, with
+            # the residual term summed inside the LN kernel (no addmm C-copy, no add pass)
+            dfin = du @ w1
             dz1, do = Fx.ln_bwd(dfin, None, z1, m1, r1, g1, p_h, rng, s1, want_dz=True, want_dy=True,
-                                dgamma=_acc(g1), dbeta=_acc(b1), dbias=_acc(o_b))
+                                dgamma=_acc(g1), dbeta=_acc(b1), dbias=_acc(o_b), dout2=dz2)
             for p in (g1, b1, o_b):
                 grad_done(p)
         emit_wgrad(o_w, do, actx)

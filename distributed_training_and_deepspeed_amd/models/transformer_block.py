@@ -19,6 +19,8 @@ from dataclasses import dataclass
 import torch
 from torch import nn
 
+from ..ops.functional import Softmax
+
 
 class MatMul(nn.Module):
     """nn.Module wrapper for torch.bmm (so its output is visible to forward hooks)."""
@@ -54,7 +56,7 @@ class TransformerBlock(nn.Module):
         self.q_proj = nn.Linear(h, h, bias=b)
         self.out_proj = nn.Linear(h, h, bias=b)
         self.compute_attention_weights = MatMul()
-        self.attention_weights_softmax = nn.Softmax(dim=-1)
+        self.attention_weights_softmax = Softmax(dim=-1)   # HIP row-softmax kernel on the GPU
         self.attention_weights_dropout = nn.Dropout(config.dropout)
         self.compute_attentions = MatMul()
         self.attention_output_dropout = nn.Dropout(config.dropout)

@@ -31,7 +31,7 @@ _SIGS = {
     # norm.hip
     "dtd_ln_bwd_num_partials": (I, [I, I]),
     "dtd_ln_fwd": (I, [I, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, P]),
-    "dtd_ln_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, F, P, U32, P]),
+    "dtd_ln_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, P, I, I, F, P, U32, P]),
     # act.hip
     "dtd_act_fwd": (I, [I, P, P, SZ, I, P]),
     "dtd_act_bwd_num_partials": (I, [I, I]),
@@ -56,6 +56,9 @@ _SIGS = {
     "dtd_attn_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, U32, P]),
     "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
     "dtd_attn_masks": (I, [P, I, I, I, F, P, U32, P]),
+    # softmax.hip
+    "dtd_softmax_fwd": (I, [I, P, P, I, I, P]),
+    "dtd_softmax_bwd": (I, [I, P, P, P, I, I, P]),
     # reduce.hip
     "dtd_splitk_reduce": (I, [P, I, I, ctypes.c_longlong, P, I, I, P]),
 }

@@ -6,7 +6,7 @@
 //
 //   forward :  z   = r + dropout(y)            (y or r may be absent)
 //              out = (z - mean) * rstd * gamma + beta
-//   backward:  dz  = rstd * (g - mean(g) - xhat * mean(g * xhat)) + dz_extra,  g = dout * gamma
+//   backward:  dz  = rstd * (g - mean(g) - xhat * mean(g * xhat)) + dz_extra,  g = (dout + dout2) * gamma
 //              dy  = dropout_bwd(dz)                              (mask regenerated, not stored)
 //              column partials of dout*xhat (dgamma), dout (dbeta), dy (bias of y's producer)
 //
@@ -29,7 +29,8 @@ struct LnFwdArgs {
 };
 
 struct LnBwdArgs {
-  const void* dout; const void* dz_extra; const void* z; const float* mean; const float* rstd;
+  const void* dout; const void* dout2;  // dout2: optional second upstream gradient term
+  const void* dz_extra; const void* z; const float* mean; const float* rstd;
   const void* gamma; void* dz; void* dy; float* part_gamma; float* part_beta; float* part_bias;
   int rows, h; float p; const uint64_t* rng; uint32_t stream_id;
 };
@@ -144,6 +145,12 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
       float zz[VEC], dd[VEC];
       vload<T, VEC>((const T*)a.z + base + col, zz);
       vload<T, VEC>((const T*)a.dout + base + col, dd);
+      if (a.dout2) {
+        float e[VEC];
+        vload<T, VEC>((const T*)a.dout2 + base + col, e);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) dd[j] += e[j];
+      }
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         const int i = c * VEC + j;
@@ -291,6 +298,7 @@ __global__ void __launch_bounds__(256) ln_bwd_block(LnBwdArgs a) {
       float zz[2], dd[2], gm[2];
       vload<T, 2>((const T*)a.z + base + col, zz);
       vload<T, 2>((const T*)a.dout + base + col, dd);
+      if (a.dout2) { float e[2]; vload<T, 2>((const T*)a.dout2 + base + col, e); dd[0] += e[0]; dd[1] += e[1]; }
       vload<T, 2>((const T*)a.gamma + col, gm);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -305,6 +313,7 @@ __global__ void __launch_bounds__(256) ln_bwd_block(LnBwdArgs a) {
       float zz[2], dd[2], gm[2], dz[2];
       vload<T, 2>((const T*)a.z + base + col, zz);
       vload<T, 2>((const T*)a.dout + base + col, dd);
+      if (a.dout2) { float e[2]; vload<T, 2>((const T*)a.dout2 + base + col, e); dd[0] += e[0]; dd[1] += e[1]; }
       vload<T, 2>((const T*)a.gamma + col, gm);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -345,9 +354,15 @@ void dispatch(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream
   if (try_wave<T, 2, 1>(f, b, nblocks_bwd, s)) return;      // h = 128
   if (try_wave<T, 4, 1>(f, b, nblocks_bwd, s)) return;      // 256
   if (try_wave<T, 8, 1>(f, b, nblocks_bwd, s)) return;      // 512
-  if (try_wave<T, 8, 3, 32>(f, b, nblocks_bwd, s)) return;  // 768: two rows per wave, 16 B/lane
-  if (try_wave<T, 8, 2>(f, b, nblocks_bwd, s)) return;      // 1024
-  if (try_wave<T, 8, 5, 32>(f, b, nblocks_bwd, s)) return;  // 1280: two rows per wave
+  // h = 768 / 1280: the forward moves two rows per wave in 16-byte vectors (faster: 23.2 ->
+  // 19.8 us at 16k x 768); the backward keeps one row per wave (8-byte vectors) because its
+  // per-lane state (x-hat, g, 3 partial arrays) doubles with two rows and costs occupancy
+  // (24.4 -> 31.3 us measured).
+  if (f && try_wave<T, 8, 3, 32>(f, b, nblocks_bwd, s)) return;   // 768 fwd
+  if (!f && try_wave<T, 4, 3>(f, b, nblocks_bwd, s)) return;      // 768 bwd
+  if (try_wave<T, 8, 2>(f, b, nblocks_bwd, s)) return;            // 1024
+  if (f && try_wave<T, 8, 5, 32>(f, b, nblocks_bwd, s)) return;   // 1280 fwd
+  if (!f && try_wave<T, 4, 5>(f, b, nblocks_bwd, s)) return;      // 1280 bwd
   if (try_wave<T, 8, 3>(f, b, nblocks_bwd, s)) return;      // 1536
   if (try_wave<T, 8, 4>(f, b, nblocks_bwd, s)) return;      // 2048
   if (f) hipLaunchKernelGGL((ln_fwd_block<T>), dim3(f->rows), dim3(256), 0, s, *f);
@@ -380,12 +395,12 @@ DTD_EXPORT int dtd_ln_fwd(int dtype, const void* y, const void* r, const void* g
   DTD_LAUNCH_CHECK();
 }
 
-DTD_EXPORT int dtd_ln_bwd(int dtype, const void* dout, const void* dz_extra, const void* z,
+DTD_EXPORT int dtd_ln_bwd(int dtype, const void* dout, const void* dout2, const void* dz_extra, const void* z,
                           const float* mean, const float* rstd, const void* gamma, void* dz, void* dy,
                           float* part_gamma, float* part_beta, float* part_bias, int rows, int h,
                           float p, const uint64_t* rng, uint32_t stream_id, hipStream_t s) {
   if (rows <= 0) return 0;
-  LnBwdArgs a{dout, dz_extra, z, mean, rstd, gamma, dz, dy, part_gamma, part_beta, part_bias,
+  LnBwdArgs a{dout, dout2, dz_extra, z, mean, rstd, gamma, dz, dy, part_gamma, part_beta, part_bias,
               rows, h, p, rng, stream_id};
   const int nb = dtd_ln_bwd_num_partials(rows, h);
   if (dtype == kBF16) dispatch<bf16>(nullptr, &a, nb, s);

@@ -108,15 +108,18 @@ def _finalize(part: torch.Tensor, n: int, cols: int, dst, acc: bool, scale: floa
 
 def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: int,
            want_dz: bool = True, want_dy: bool = False,
-           dgamma=None, dbeta=None, dbias=None, acc: bool = False):
+           dgamma=None, dbeta=None, dbias=None, acc: bool = False, dout2=None):
     """Backward of ``ln_fwd``.  Returns (dz, dy); writes dgamma/dbeta/dbias (bias of the
-    producer of y, i.e. column sums of dy) into the destination tensors."""
+    producer of y, i.e. column sums of dy) into the destination tensors.  ``dout2``: a second
+    upstream gradient summed into ``dout`` inside the kernel (residual branches)."""
     rows = dout.numel() // dout.shape[-1]
     h = dout.shape[-1]
     if not _on_gpu(dout):
         zf = z.float().view(rows, h)
         xh = (zf - mean[:, None]) * rstd[:, None]
         d = dout.float().view(rows, h)
+        if dout2 is not None:
+            d = d + dout2.float().view(rows, h)
         g = d * gamma.float()
         m1 = g.mean(-1, keepdim=True)
         m2 = (g * xh).mean(-1, keepdim=True)
@@ -131,7 +134,7 @@ def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: i
         _write_grad(dgamma, (d * xh).sum(0), acc)
         _write_grad(dbeta, d.sum(0), acc)
         return (dz.to(dout.dtype).view_as(dout) if want_dz else None), dy
-    dout, dz_extra = _c(dout), _c(dz_extra)
+    dout, dz_extra, dout2 = _c(dout), _c(dz_extra), _c(dout2)
     dz = torch.empty_like(dout) if want_dz else None
     dy = torch.empty_like(dout) if want_dy else None
     n = _lib.lib().dtd_ln_bwd_num_partials(rows, h)
@@ -141,7 +144,8 @@ def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: i
     pg = part[next(slots)] if dgamma is not None else None
     pb = part[next(slots)] if dbeta is not None else None
     py = part[next(slots)] if (dbias is not None and want_dy) else None
-    _lib.call("dtd_ln_bwd", _lib.dt(dout), dout.data_ptr(), _lib.ptr(dz_extra), z.data_ptr(), mean.data_ptr(),
+    _lib.call("dtd_ln_bwd", _lib.dt(dout), dout.data_ptr(), _lib.ptr(dout2), _lib.ptr(dz_extra), z.data_ptr(),
+              mean.data_ptr(),
               rstd.data_ptr(), gamma.data_ptr(), _lib.ptr(dz), _lib.ptr(dy), _lib.ptr(pg), _lib.ptr(pb),
               _lib.ptr(py), rows, h, float(p if want_dy else 0.0), rng.state.data_ptr(), sid, _lib.stream())
     dsts = [d for d, on in ((dgamma, pg is not None), (dbeta, pb is not None), (dbias, py is not None)) if on]
@@ -365,3 +369,54 @@ def sq_norm(x: torch.Tensor) -> torch.Tensor:
     part = torch.empty(n, dtype=torch.float32, device=x.device)
     _lib.call("dtd_sqnorm_partials", x.data_ptr(), _lib.dt(x), x.numel(), part.data_ptr(), _lib.stream())
     return part.sum()
+
+
+# --------------------------------------------------------------------------------------
+# row softmax (instrumented block)
+# --------------------------------------------------------------------------------------
+def softmax_fwd(x: torch.Tensor) -> torch.Tensor:
+    if not _on_gpu(x) or x.dtype not in (torch.bfloat16, torch.float32):
+        return torch.softmax(x.float(), dim=-1).to(x.dtype)
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    n = x.shape[-1]
+    _lib.call("dtd_softmax_fwd", _lib.dt(x), x.data_ptr(), y.data_ptr(), x.numel() // n, n, _lib.stream())
+    return y
+
+
+def softmax_bwd(y: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    if not _on_gpu(y) or y.dtype not in (torch.bfloat16, torch.float32):
+        yf, df = y.float(), dy.float()
+        return (yf * (df - (yf * df).sum(-1, keepdim=True))).to(y.dtype)
+    dy = dy.contiguous().to(y.dtype)
+    dx = torch.empty_like(y)
+    n = y.shape[-1]
+    _lib.call("dtd_softmax_bwd", _lib.dt(y), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // n, n,
+              _lib.stream())
+    return dx
+
+
+class _SoftmaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = softmax_fwd(x)
+        ctx.save_for_backward(y)      # like ATen's softmax: the output is the saved activation
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return softmax_bwd(y, dy)
+
+
+class Softmax(torch.nn.Module):
+    """Drop-in ``nn.Softmax(dim=-1)`` backed by the HIP row-softmax kernels on the GPU."""
+
+    def __init__(self, dim: int = -1):
+        super().__init__()
+        if dim not in (-1,):
+            raise ValueError("row softmax over the last dim only")
+        self.dim = dim
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return _SoftmaxFn.apply(x)

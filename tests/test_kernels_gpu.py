@@ -58,6 +58,7 @@ def test_layernorm_fwd_bwd(h, dtype):
     beta = (0.1 * torch.randn(h)).to(dtype)
     dout = torch.randn(rows, h, dtype=dtype)
     dext = torch.randn(rows, h, dtype=dtype)
+    dout2 = torch.randn(rows, h, dtype=dtype) if h != 384 else None   # second upstream term
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
     outs = {}
     for dev, rng in ((DEV, g), ("cpu", c)):
@@ -66,7 +67,8 @@ def test_layernorm_fwd_bwd(h, dtype):
         db = torch.zeros(h, dtype=torch.float32, device=dev)
         dbias = torch.zeros(h, dtype=torch.float32, device=dev)
         dz, dy = Fx.ln_bwd(dout.to(dev), dext.to(dev), z, m, rs, gamma.to(dev), 0.1, rng, 5, want_dz=True,
-                           want_dy=True, dgamma=dg, dbeta=db, dbias=dbias)
+                           want_dy=True, dgamma=dg, dbeta=db, dbias=dbias,
+                           dout2=None if dout2 is None else dout2.to(dev))
         outs[dev] = (z, o, m, rs, dz, dy, dg, db, dbias)
     for a, b in zip(outs[DEV], outs["cpu"]):
         close(a, b, tol)
@@ -188,3 +190,17 @@ def test_split_k_wgrad_matches_fp32():
     close(w.grad, ref, 1e-2)
     emit_wgrad(w, dy, x)               # second contribution accumulates
     close(w.grad, 2 * ref, 1e-2)
+
+
+@pytest.mark.parametrize("n", [512, 100, 4096, 8200])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_row_softmax_fwd_bwd(n, dtype):
+    torch.manual_seed(3)
+    x = (3 * torch.randn(37, n)).to(dtype)
+    dy = torch.randn(37, n).to(dtype)
+    y = Fx.softmax_fwd(x.to(DEV))
+    ref = torch.softmax(x.float(), -1)
+    close(y, ref, 2e-2 if dtype == torch.bfloat16 else 1e-5)
+    dx = Fx.softmax_bwd(y, dy.to(DEV))
+    rdx = ref * (dy.float() - (ref * dy.float()).sum(-1, keepdim=True))
+    close(dx, rdx, 3e-2 if dtype == torch.bfloat16 else 1e-4)

@@ -133,3 +133,33 @@ def test_comm_busbw_factors():
     assert _busbw_factor("all_reduce", 8) == pytest.approx(2 * 7 / 8)
     assert _busbw_factor("reduce_scatter_tensor", 8) == pytest.approx(7 / 8)
     assert _busbw_factor("all_gather_into_tensor", 4) == pytest.approx(3 / 4)
+
+
+def test_replicated_checkpoint_resume_is_exact(tmp_path):
+    from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
+    from distributed_training_and_deepspeed_amd.models import build_model
+    from distributed_training_and_deepspeed_amd.optim import hf_adamw
+    from distributed_training_and_deepspeed_amd.utils.checkpoint import load_checkpoint, save_checkpoint
+    ds = SyntheticLMDataset(build_model("tiny").cfg, 8, seq_len=32, seed=4)
+
+    def step(m, o, i):
+        m(ds.input_ids[2 * i:2 * i + 2], labels=ds.labels[2 * i:2 * i + 2]).loss.backward()
+        o.step()
+        o.zero_grad()
+        m.rt.rng.advance()
+
+    a = build_model("tiny", seed=3)
+    oa = hf_adamw(a.parameters(), lr=1e-3)
+    for i in range(2):
+        step(a, oa, i)
+    save_checkpoint(str(tmp_path / "ck.pt"), a, oa, step=2, extra={"note": "x"})
+    for i in range(2, 4):
+        step(a, oa, i)
+    b = build_model("tiny", seed=11)
+    ob = hf_adamw(b.parameters(), lr=1e-3)
+    meta = load_checkpoint(str(tmp_path / "ck.pt"), b, ob)
+    assert meta == {"step": 2, "extra": {"note": "x"}}
+    for i in range(2, 4):
+        step(b, ob, i)
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        assert torch.equal(p, q), n
