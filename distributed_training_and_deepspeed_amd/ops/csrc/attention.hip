@@ -141,6 +141,19 @@ __global__ void __launch_bounds__(256) attn_mask_kernel(uint32_t* __restrict__ m
   }
 }
 
+// XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs, each with its own
+// L2; in HW order the gridDim.x tiles of one (batch, head) -- which all stream the same K/V
+// (dK/dV: Q/dO) -- would land on gridDim.x different XCDs and fetch those operands once per XCD.
+// Renumber so each XCD runs a contiguous range of tiles: the tiles of a head share one L2.
+__device__ __forceinline__ void xcd_tile(int& tx, int& ty) {
+  const int nx = gridDim.x, n = nx * gridDim.y;
+  const int L = blockIdx.x + nx * blockIdx.y;
+  if (n % 8) { tx = blockIdx.x; ty = blockIdx.y; return; }
+  const int T = (L % 8) * (n / 8) + L / 8;
+  tx = T % nx;
+  ty = T / nx;
+}
+
 // Stage a [rows x D] bf16 tile (row stride `ld` in global) into registers, then LDS.
 template <int D, int ROWS>
 struct TileLoader {
@@ -175,9 +188,11 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * VP];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, r = lane & 31;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  int tx, ty;
+  xcd_tile(tx, ty);
+  const int bh = ty, b = bh / a.H, h = bh % a.H;
   const int S = a.S;
-  const int qblk = blockIdx.x * 128, q0 = qblk + w * 32;
+  const int qblk = tx * 128, q0 = qblk + w * 32;
   const int q = q0 + r;
   const bool qvalid = q < S;
   const float sl2 = a.slopes ? a.slopes[h] * kLog2e : 0.f;
@@ -325,9 +340,11 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   __shared__ float lse_s[2][BM], del_s[2][BM];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, r = lane & 31;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  int tx, ty;
+  xcd_tile(tx, ty);
+  const int bh = ty, b = bh / a.H, h = bh % a.H;
   const int S = a.S;
-  const int kblk = blockIdx.x * 128;
+  const int kblk = tx * 128;
   const int key = kblk + w * 32 + r;
   const bool kvalid = key < S;
   const float sl2 = a.slopes ? a.slopes[h] * kLog2e : 0.f;
@@ -442,9 +459,11 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * KP];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, r = lane & 31;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  int tx, ty;
+  xcd_tile(tx, ty);
+  const int bh = ty, b = bh / a.H, h = bh % a.H;
   const int S = a.S;
-  const int qblk = blockIdx.x * 128, q0 = qblk + w * 32;
+  const int qblk = tx * 128, q0 = qblk + w * 32;
   const int q = q0 + r;
   const bool qvalid = q < S;
   const float sl2 = a.slopes ? a.slopes[h] * kLog2e : 0.f;

@@ -112,10 +112,12 @@ __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
   }
 }
 
-template <typename T, int VEC, int ITERS, int LPR>
+// One row per wave (the two-rows-per-wave layout of the forward doubles this kernel's per-lane
+// state and costs occupancy).
+template <typename T, int VEC, int ITERS>
 __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
-  constexpr int NPL = VEC * ITERS, RPW = 64 / LPR;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6, sub = lane % LPR;
+  constexpr int NPL = VEC * ITERS, LPR = 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6, sub = lane;
   const int h = a.h;
   const bool has_drop = a.p > 0.f && a.dy != nullptr;
   DropoutRng g(a.rng, a.stream_id);
@@ -127,18 +129,11 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
 #pragma unroll
   for (int c = 0; c < ITERS; ++c) vload<T, VEC>((const T*)a.gamma + (c * LPR + sub) * VEC, gm + c * VEC);
 
-  // both half-waves of an LPR=32 wave run the same trip count (rows are padded by clamping and
-  // masked), so the row reductions' cross-lane shuffles always see a fully active wave
-  const int rstride = gridDim.x * nw * RPW;
-  for (int rb = (blockIdx.x * nw + w) * RPW; rb < a.rows; rb += rstride) {
-    const int row0 = rb + lane / LPR;
-    const bool valid = row0 < a.rows;
-    const int row = valid ? row0 : a.rows - 1;
+  for (int row = blockIdx.x * nw + w; row < a.rows; row += gridDim.x * nw) {
     const size_t base = (size_t)row * h;
     const float mu = a.mean[row], rs = a.rstd[row];
     float xh[NPL], dg[NPL];
     float s1 = 0.f, s2 = 0.f;
-    const float vm = valid ? 1.f : 0.f;   // padded rows contribute nothing to the partials
 #pragma unroll
     for (int c = 0; c < ITERS; ++c) {
       const int col = (c * LPR + sub) * VEC;
@@ -158,12 +153,11 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
         dg[i] = dd[j] * gm[i];
         s1 += dg[i];
         s2 += dg[i] * xh[i];
-        pg[i] += vm * dd[j] * xh[i];
-        pb[i] += vm * dd[j];
+        pg[i] += dd[j] * xh[i];
+        pb[i] += dd[j];
       }
     }
-    const float m1 = row_sum<LPR>(s1) / h, m2 = row_sum<LPR>(s2) / h;
-    if (!valid) continue;
+    const float m1 = wave_sum(s1) / h, m2 = wave_sum(s2) / h;
 #pragma unroll
     for (int c = 0; c < ITERS; ++c) {
       const int col = (c * LPR + sub) * VEC;
@@ -189,14 +183,6 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
         }
         vstore<T, VEC>((T*)a.dy + base + col, dy);
       }
-    }
-  }
-  if constexpr (LPR < 64) {   // fold the half-waves (same columns, different rows)
-#pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-      pg[i] += __shfl_xor(pg[i], 32, 64);
-      pb[i] += __shfl_xor(pb[i], 32, 64);
-      py[i] += __shfl_xor(py[i], 32, 64);
     }
   }
   // Block-level reduction of the column partials through LDS (one array at a time).
@@ -344,7 +330,7 @@ bool try_wave(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream
     hipLaunchKernelGGL((ln_fwd_wave<T, VEC, ITERS, LPR>), dim3((f->rows + rows_per_block - 1) / rows_per_block),
                        dim3(256), 0, s, *f);
   } else {
-    hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, LPR>), dim3(nblocks_bwd), dim3(256), 0, s, *b);
+    hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS>), dim3(nblocks_bwd), dim3(256), 0, s, *b);
   }
   return true;
 }
