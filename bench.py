@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--grad-dtype", default=None, choices=[None, "bf16", "fp32"])
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("DTD_BUCKET_MB", "64")))
     ap.add_argument("--impl", default="fused", choices=["fused", "reference"])
+    ap.add_argument("--graph", default="off", choices=["on", "off"],
+                    help="capture the whole training step in a hipGraph and replay it")
     ap.add_argument("--small-bucket-allreduce", default="rccl", choices=["rccl", "xgmi"],
                     help="xgmi: buckets <= 4 MiB use the native peer-mapped all-reduce kernel")
     ap.add_argument("--dense-mlm-head", action="store_true")
@@ -90,12 +92,24 @@ def main():
     labels = ds.labels.view(-1, B, S).to(device)
     nbuf = ids.shape[0]
 
-    def step(i):
-        out = ddp(ids[i % nbuf], labels=labels[i % nbuf])
+    def train_step(input_ids, labels):
+        out = ddp(input_ids, labels=labels)
         out.loss.backward()
         opt.step()
         model.rt.rng.advance()
-        return out.loss
+        return out.loss.detach()
+
+    graphed = None
+    if args.graph == "on" and cuda:
+        # one hipGraph replay per step (host-launch-bound small batches); static-size MLM head
+        from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep, mlm_capacity
+        model.rt.mlm_capacity = mlm_capacity(B * S)
+        graphed = CapturedStep(train_step, {"input_ids": ids[0], "labels": labels[0]}, warmup=3, runtime=model.rt)
+
+    def step(i):
+        if graphed is not None:
+            return graphed(input_ids=ids[i % nbuf], labels=labels[i % nbuf])
+        return train_step(ids[i % nbuf], labels[i % nbuf])
 
     def sync():
         if cuda:
@@ -113,6 +127,8 @@ def main():
         loss = step(args.warmup + i)
     sync()
     dt = time.perf_counter() - t0
+    if graphed is not None:
+        graphed.check()
     if world > 1:
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -146,6 +162,7 @@ def main():
                 "mlm_head": "dense" if args.dense_mlm_head else "sparse (labelled rows only; identical loss/grads)",
                 "optimizer": "fused AdamW (transformers.AdamW hyper-params, lr 5e-5)",
                 "tuned_gemms": tuned,
+                "hip_graph": graphed is not None,
             },
             "loss_first": round(first_loss, 4),
             "loss_last": round(float(loss.detach()), 4),

@@ -45,6 +45,10 @@ class Runtime:
         self.rng = rng or RngState(seed=0)
         self.exact_dropout = exact_dropout  # reference path uses the counter RNG masks
         self._next_sid = 1
+        # Sparse MLM head with a STATIC row capacity (graph capture: no data-dependent shapes,
+        # no host sync).  None -> exact-size gather (nonzero).  See MLMHead.loss.
+        self.mlm_capacity: int | None = None
+        self.mlm_overflow: torch.Tensor | None = None   # device flag: a batch exceeded the capacity
 
     def new_sid(self) -> int:
         """Dropout stream id for one call site; deterministic per model structure so two

@@ -163,3 +163,29 @@ def test_replicated_checkpoint_resume_is_exact(tmp_path):
         step(b, ob, i)
     for (n, p), q in zip(a.named_parameters(), b.parameters()):
         assert torch.equal(p, q), n
+
+
+def test_static_capacity_mlm_head_matches_exact_gather():
+    """The graph-capturable MLM head (static labelled-row capacity) gives the same loss and
+    gradients as the exact-size gather, and flags an over-full batch."""
+    from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
+    from distributed_training_and_deepspeed_amd.models import build_model
+    from distributed_training_and_deepspeed_amd.utils.graphs import mlm_capacity
+    ds = SyntheticLMDataset(build_model("tiny").cfg, 4, seq_len=64, seed=2)
+    res = []
+    for cap in (None, mlm_capacity(4 * 64)):
+        m = build_model("tiny", impl="fused", seed=3)
+        m.rt.mlm_capacity = cap
+        m.rt.mlm_overflow = torch.zeros((), dtype=torch.bool)
+        loss = m(ds.input_ids, labels=ds.labels).loss
+        loss.backward()
+        res.append((loss.detach(), {n: p.grad.clone() for n, p in m.named_parameters()}))
+        assert not bool(m.rt.mlm_overflow)
+    assert torch.allclose(res[0][0], res[1][0], atol=1e-6)
+    for n in res[0][1]:
+        assert torch.allclose(res[0][1][n], res[1][1][n], atol=1e-6), n
+    m = build_model("tiny", impl="fused", seed=3)
+    m.rt.mlm_capacity = 4
+    m.rt.mlm_overflow = torch.zeros((), dtype=torch.bool)
+    m(ds.input_ids, labels=ds.labels)
+    assert bool(m.rt.mlm_overflow)
