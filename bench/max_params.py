@@ -1,0 +1,152 @@
+#!/usr/bin/env python
+"""Largest trainable model per ZeRO stage on MI355X (the "max params via ZeRO" half of the
+headline metric, BASELINE.json; reference: zero_dp_training.py stages 0-3 + the memory
+estimator of estimate_transformer_memory.py).
+
+1. Projection: for each (world size, ZeRO stage), the largest GPT-style model (pre-LN,
+   heads = h/128, ffn = 4h, GPT-2 vocab) whose per-GPU training memory -- bf16 weights and
+   grads, fp32 master + Adam moments (16 B/param before partitioning), flash-attention
+   activations at micro-batch 1 x 512 -- fits ``--fraction`` of the 288 GB HBM3E.
+2. ``--measure``: build that model for the LOCAL world size directly on the GPU (bf16, random
+   init), wrap it in the ZeRO engine (stage ``--stage``), run ``--steps`` full training steps
+   (forward, backward, reduce-scatter, fused Adam, all-gather) and report the allocator's peak
+   against the projection, plus tokens/s.  One JSON line.
+
+  python bench/max_params.py                         # projection table (1 and 8 GPUs)
+  python bench/max_params.py --measure --stage 3     # largest 1-GPU model, trained for real
+  torchrun --nproc-per-node 8 bench/max_params.py --measure --stage 3
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from distributed_training_and_deepspeed_amd.memory.estimate import (MI355X_HBM_BYTES,  # noqa: E402
+                                                                    project_training_memory)
+
+LAYERS = (24, 32, 40, 48, 56, 64, 80, 96, 112, 128)
+VOCAB = 50257
+
+
+def candidates():
+    for L in LAYERS:
+        for h in range(1024, 24576 + 1, 256):
+            if h % 128 == 0:
+                yield L, h
+
+
+def embed_params(h: int, positions: int = 2048) -> int:
+    return VOCAB * h + positions * h + 2 * h          # tied LM head
+
+
+def largest(world: int, stage: int, fraction: float, seq_len: int = 512, batch: int = 1):
+    best = None
+    cap = MI355X_HBM_BYTES * fraction
+    for L, h in candidates():
+        pr = project_training_memory(L, h, h // 128, batch, seq_len, precision="bf16", zero_stage=stage,
+                                     world_size=world, extra_params=embed_params(h))
+        # + the logits of one micro-batch (bf16 + fp32 LSE path) and one gathered ZeRO-3 unit
+        extra = batch * seq_len * VOCAB * 2 * 2 + (12 * h * h * 2 if stage == 3 else 0)
+        if pr.total + extra <= cap and (best is None or pr.params > best[2].params):
+            best = (L, h, pr, extra)
+    return best
+
+
+def projection_table(fraction: float) -> list[dict]:
+    rows = []
+    for world in (1, 8):
+        for stage in (0, 1, 2, 3):
+            b = largest(world, stage, fraction)
+            if b is None:
+                continue
+            L, h, pr, extra = b
+            rows.append({"world": world, "stage": stage, "layers": L, "hidden": h, "params_B": round(pr.params / 1e9, 2),
+                         "projected_GB_per_gpu": round((pr.total + extra) / 1e9, 1)})
+    return rows
+
+
+def measure(a) -> dict:
+    from distributed_training_and_deepspeed_amd import comm
+    from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
+    from distributed_training_and_deepspeed_amd.models.causal_lm import CausalLM
+    from distributed_training_and_deepspeed_amd.models.config import GPT2_MEDIUM
+    from distributed_training_and_deepspeed_amd.models.transformer import Runtime
+    from distributed_training_and_deepspeed_amd.ops.rng import RngState
+    from distributed_training_and_deepspeed_amd.parallel.zero import initialize
+    comm.init()
+    world, rank = comm.world_size(), comm.rank()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if a.layers and a.hidden:
+        L, h = a.layers, a.hidden
+    else:
+        L, h, _, _ = largest(world, a.stage, a.fraction)
+    cfg = GPT2_MEDIUM.with_(name=f"gpt-L{L}-h{h}", num_layers=L, hidden_size=h, num_heads=h // 128, ffn_size=4 * h,
+                            max_positions=2048)
+    torch.manual_seed(0)
+    t0 = time.time()
+    with torch.device(dev):                       # allocate + initialise directly in HBM
+        model = CausalLM(cfg, rt=Runtime(impl="fused", rng=RngState(seed=0, device=dev)))
+    model = model.to(torch.bfloat16)
+    n = sum(p.numel() for p in model.parameters())
+    conf = {"optimizer": {"type": "Adam", "params": {"lr": 1e-4}},
+            "zero_optimization": {"stage": a.stage, "reduce_bucket_size": 5e8}}
+    eng, opt, _, _ = initialize(model=model, model_parameters=model.parameters(), config=conf)
+    build_s = time.time() - t0
+    ds = SyntheticLMDataset(cfg, a.steps + 1, seq_len=a.seq_len, mlm=False, seed=rank)
+    ids, lab = ds.input_ids.to(dev), ds.labels.to(dev)
+    losses = []
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    t1 = None
+    for i in range(a.steps + 1):
+        if i == 1:
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+        loss = eng(ids[i:i + 1], labels=lab[i:i + 1]).loss
+        eng.backward(loss)
+        eng.step()
+        losses.append(loss.detach())
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t1
+    peak = torch.cuda.max_memory_allocated()
+    pr = project_training_memory(L, h, h // 128, 1, a.seq_len, precision="bf16", zero_stage=a.stage,
+                                 world_size=world, extra_params=embed_params(h))
+    res = {"metric": "max trainable params (ZeRO, one training step measured)", "params": n,
+           "params_B": round(n / 1e9, 3), "layers": L, "hidden": h, "stage": a.stage, "world": world,
+           "peak_alloc_GB": round(peak / 1e9, 1), "projected_GB": round(pr.total / 1e9, 1),
+           "hbm_GB": round(torch.cuda.get_device_properties(dev).total_memory / 1e9, 1),
+           "tokens_per_s": round(world * a.steps * a.seq_len / dt, 1), "build_s": round(build_s, 1),
+           "loss_first": round(float(losses[0]), 4), "loss_last": round(float(losses[-1]), 4),
+           "finite": bool(all(torch.isfinite(x) for x in losses))}
+    comm.destroy()
+    return res
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--fraction", type=float, default=0.92, help="usable share of HBM (allocator slack)")
+    p.add_argument("--measure", action="store_true")
+    p.add_argument("--stage", type=int, default=3)
+    p.add_argument("--layers", type=int, default=0)
+    p.add_argument("--hidden", type=int, default=0)
+    p.add_argument("--steps", type=int, default=2)
+    p.add_argument("--seq-len", type=int, default=512)
+    a = p.parse_args(argv)
+    if not a.measure:
+        for r in projection_table(a.fraction):
+            print(json.dumps(r))
+        return
+    res = measure(a)
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -70,6 +70,16 @@ __device__ __forceinline__ bf16x8 tr_operand(const bf16* tile, int stride, int r
   return cat(tr_read(p), tr_read(p + 8 * stride));
 }
 
+// Raw v_exp_f32 (2^x): the softmax arguments are <= 0, so the libm wrapper's denormal
+// range handling (extra VALU per element) is not needed -- tiny results flush to 0.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// Dropout as a bit select: all-ones / zero lane mask from bit `b` of `w` (one v_bfe_i32), AND-ed
+// into the float's bits -- 2 VALU per element instead of shift/compare/select/multiply; the
+// 1/(1-p) rescale is folded into the per-row epilogue.
+__device__ __forceinline__ float keep_bits(float v, uint32_t w, int b) {
+  return __int_as_float(__float_as_int(v) & __builtin_amdgcn_sbfe((int)w, b, 1));
+}
+
 __device__ __forceinline__ float keep_of(const DropoutRng& g, uint64_t e, uint32_t thr) {
   const uint32_t b = g.bits(e >> 1);
   const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
@@ -236,28 +246,42 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
         acc = mfma32(*reinterpret_cast<const bf16x8*>(&K[(kb * 32 + r) * KP + 16 * c + 8 * hh]), qf[c], acc);
       sacc[kb] = acc;
     }
+    // log2-domain scores.  Fast path (no ALiBi, interior tile): the row max is taken on the raw
+    // accumulator (scale > 0) and the scale is folded into the exponent's FMA -- 4 VALU per score
+    // incl. the running sum, vs 10+ with a per-element scale/bias/mask pass.
     const bool needmask = (k0 + BN > S) || (a.causal && k0 + BN - 1 > q0);
+    const bool slow = needmask || sl2 != 0.f;
     float tmax = -INFINITY;
+    if (slow) {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = k0 + kb * 32 + crow(i, hh);
-        float s = fmaf(sacc[kb][i], sc2, sl2 * (float)key);
-        if (needmask && (key >= S || (a.causal && key > q))) s = -INFINITY;
-        sacc[kb][i] = s;
-        tmax = fmaxf(tmax, s);
-      }
+        for (int i = 0; i < 16; ++i) {
+          const int key = k0 + kb * 32 + crow(i, hh);
+          float s = fmaf(sacc[kb][i], sc2, sl2 * (float)key);
+          if (needmask && (key >= S || (a.causal && key > q))) s = -INFINITY;
+          sacc[kb][i] = s;
+          tmax = fmaxf(tmax, s);
+        }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, sacc[kb][i]);
+      tmax *= sc2;
+    }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mnew);  // m = -inf on the first tile -> 0
+    const float alpha = fexp2(m - mnew);  // m = -inf on the first tile -> 0
     m = mnew;
+    const float mexp = mnew == -INFINITY ? 0.f : mnew;
+    const float msc = slow ? 1.f : sc2;
     float psum = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float pv = exp2f(sacc[kb][i] - mnew);
+        const float pv = fexp2(fmaf(sacc[kb][i], msc, -mexp));
         psum += pv;
         sacc[kb][i] = pv;
       }
@@ -273,7 +297,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
         const int kw = (k0 >> 5) + kb;
         const uint32_t mw = kw < a.W ? mcol[(size_t)kw * S] : 0u;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[kb][i] *= ((mw >> crow(i, hh)) & 1u) ? inv_keep : 0.f;
+        for (int i = 0; i < 16; ++i) sacc[kb][i] = keep_bits(sacc[kb][i], mw, crow(i, hh));
       }
     }
     // O^T += V^T . P^T: the score accumulator is the B operand; V^T comes from transposed reads
@@ -291,7 +315,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     __syncthreads();
   }
   if (!qvalid) return;
-  const float inv_l = l > 0.f ? 1.f / l : 0.f;
+  const float inv_l = l > 0.f ? inv_keep / l : 0.f;   // dropout 1/(1-p) folded in here
   bf16* op = a.o + (size_t)(b * S + q) * a.ldo + h * D;
 #pragma unroll
   for (int d = 0; d < NDB; ++d)
@@ -351,6 +375,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   const float sc2 = a.scale * kLog2e;
   const bool drop = a.maskB != nullptr;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
+  const float kbias = sl2 * (float)key;   // ALiBi bias of this lane's key (0 without ALiBi)
   const uint32_t* mcol = drop ? a.maskB + (size_t)bh * a.W * S + (kvalid ? key : 0) : nullptr;
   const bf16* qbase = a.q + (size_t)b * S * a.ld + h * D;
   const bf16* obase = a.dout + (size_t)b * S * a.ldo + h * D;
@@ -407,13 +432,18 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qr = qb * 32 + crow(i, hh);
-        const int qq = q0 + qr;
-        const float s = fmaf(sacc[i], sc2, sl2 * (float)key - lse_s[buf][qr]);
-        float pv = exp2f(s);
-        if (needmask && (!kvalid || qq >= S || (a.causal && key > qq))) pv = 0.f;
-        const float keep = drop ? (((mw >> crow(i, hh)) & 1u) ? inv_keep : 0.f) : 1.f;
-        sacc[i] = pv * keep;                                  // dropped P (for dV)
-        pacc[i] = pv * (pacc[i] * keep - del_s[buf][qr]);     // dS
+        float pv = fexp2(fmaf(sacc[i], sc2, kbias - lse_s[buf][qr]));
+        if (needmask) {
+          const int qq = q0 + qr;
+          if (!kvalid || qq >= S || (a.causal && key > qq)) pv = 0.f;
+        }
+        if (drop) {
+          sacc[i] = keep_bits(pv, mw, crow(i, hh));           // dropped P (x 1/(1-p) at the end)
+          pacc[i] = pv * fmaf(keep_bits(pacc[i], mw, crow(i, hh)), inv_keep, -del_s[buf][qr]);  // dS
+        } else {
+          sacc[i] = pv;
+          pacc[i] = pv * (pacc[i] - del_s[buf][qr]);
+        }
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -435,6 +465,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
     __syncthreads();
   }
   if (!kvalid) return;
+  const float dv_scale = inv_keep;   // the dropped P fed to dV carried keep bits only
   bf16* dkp = a.dk + (size_t)(b * S + key) * a.ld + h * D;
   bf16* dvp = a.dv + (size_t)(b * S + key) * a.ld + h * D;
 #pragma unroll
@@ -443,7 +474,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
     for (int gq = 0; gq < 4; ++gq) {
       bf16x4 k4, v4;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) { k4[t] = (bf16)(dk[d][4 * gq + t] * a.scale); v4[t] = (bf16)dv[d][4 * gq + t]; }
+      for (int t = 0; t < 4; ++t) { k4[t] = (bf16)(dk[d][4 * gq + t] * a.scale); v4[t] = (bf16)(dv[d][4 * gq + t] * dv_scale); }
       *reinterpret_cast<bf16x4*>(dkp + d * 32 + 8 * gq + 4 * hh) = k4;
       *reinterpret_cast<bf16x4*>(dvp + d * 32 + 8 * gq + 4 * hh) = v4;
     }
@@ -514,13 +545,26 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
       }
       const int kw = (k0 >> 5) + kb;
       const uint32_t mw = drop && kw < a.W ? mcol[(size_t)kw * S] : 0u;
+      // P = exp2(s*log2e - lse): 2 VALU on interior tiles without ALiBi
+      if (needmask || sl2 != 0.f) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = k0 + kb * 32 + crow(i, hh);
-        float pv = exp2f(fmaf(sacc[i], sc2, sl2 * (float)key - lse2));
-        if (needmask && (!qvalid || key >= S || (a.causal && key > q))) pv = 0.f;
-        const float keep = drop ? (((mw >> crow(i, hh)) & 1u) ? inv_keep : 0.f) : 1.f;
-        sacc[i] = pv * (pacc[i] * keep - dl);  // dS^T
+        for (int i = 0; i < 16; ++i) {
+          const int key = k0 + kb * 32 + crow(i, hh);
+          float pv = fexp2(fmaf(sacc[i], sc2, sl2 * (float)key - lse2));
+          if (needmask && (!qvalid || key >= S || (a.causal && key > q))) pv = 0.f;
+          sacc[i] = pv;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = fexp2(fmaf(sacc[i], sc2, -lse2));
+      }
+      // dS^T = P * (dP - delta), dP = dropout(dP') (keep bit, 1/(1-p))
+      if (drop) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] *= fmaf(keep_bits(pacc[i], mw, crow(i, hh)), inv_keep, -dl);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] *= pacc[i] - dl;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {

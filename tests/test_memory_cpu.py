@@ -51,3 +51,15 @@ def test_instrumented_block_equals_fused_layer():
     blk.eval()
     x = torch.randn(2, 16, 64)
     assert torch.allclose(layer(x), blk(x), atol=1e-5)
+
+
+def test_max_params_projection_grows_with_zero_stage():
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench"))
+    import max_params
+    rows = {(r["world"], r["stage"]): r for r in max_params.projection_table(0.92)}
+    assert rows[(1, 0)]["params_B"] > 10                       # 16 B/param: >10 B params in 288 GB
+    p8 = [rows[(8, s)]["params_B"] for s in range(4)]
+    assert p8 == sorted(p8) and p8[3] > 5 * p8[0]               # partitioning multiplies capacity
+    assert all(r["projected_GB_per_gpu"] <= 0.92 * 288 * 1.0737 for r in rows.values())
