@@ -169,6 +169,47 @@ class GPipe(nn.Module):
     def local_value(self):  # torch Pipe returned an RRef; kept for script-level parity
         return self
 
+    def train_step(self, x: torch.Tensor, target: torch.Tensor, loss_fn, schedule: str = "1f1b") -> torch.Tensor:
+        """Forward + backward of one mini-batch; returns the loss (mean over micro-batches).
+
+        ``1f1b``: after S-1 warm-up forwards, every new micro-batch forward is followed by the
+        backward of the oldest one, so at most S micro-batches hold activations at a time
+        (GPipe fill-drain keeps all ``chunks``, which is why torch Pipe checkpoints them).
+        Backward of micro-batch m on stage s and forward of m+S-1 on stage 0 run on different
+        devices and overlap.  ``gpipe``: all forwards, then all backwards.  The loss of each
+        micro-batch is ``loss_fn(out, target_chunk) / chunks`` (micro-batch mean)."""
+        if schedule not in ("1f1b", "gpipe"):
+            raise ValueError(schedule)
+        mx = list(torch.chunk(x, self.chunks, dim=0))
+        mt = list(torch.chunk(target, self.chunks, dim=0))
+        n, S = len(mx), len(self.stages)
+        pending, total = [], None
+
+        def fwd(m):
+            h = mx[m]
+            for s in range(S):
+                h = send_to(h, self.devices[s]) if torch.is_tensor(h) else h
+                with torch.cuda.device(self.devices[s]) if self.devices[s].type == "cuda" else _null():
+                    h = self._run(s, m, h)
+            loss = loss_fn(h, mt[m].to(h.device)) / n
+            pending.append(loss)
+            return loss.detach()
+
+        def bwd():
+            pending.pop(0).backward()
+
+        warm = n if schedule == "gpipe" else min(S - 1, n)
+        for m in range(n):
+            ls = fwd(m)
+            total = ls if total is None else total + ls.to(total.device)
+            if m >= warm:
+                bwd()
+        while pending:
+            bwd()
+        if self.set_micro is not None:
+            self.set_micro(0)
+        return total
+
 
 class _null:
     def __enter__(self):

@@ -56,6 +56,8 @@ def main():
     parser.add_argument("--timing", default="device", choices=["device", "host"])
     parser.add_argument("--checkpoint", default="except_last", choices=["except_last", "always", "never"])
     parser.add_argument("--impl", default="auto", choices=["auto", "fused", "reference"])
+    parser.add_argument("--schedule", default="gpipe", choices=["gpipe", "1f1b"],
+                        help="pipeline schedule: torch-Pipe fill-drain (reference) or 1F1B (S live micro-batches)")
     args = parser.parse_args()
 
     config = get_config(args.model)
@@ -84,10 +86,15 @@ def main():
     n, loss = 0, None
     for batch in loader:
         input_ids = batch["input_ids"]
-        outputs = model(input_ids)
-        labels = batch["labels"].to(bert.head_device)
-        loss = loss_fn(outputs.view(-1, config.vocab_size).float(), labels.view(-1))
-        loss.backward()
+        if args.pipeline and args.schedule == "1f1b":
+            loss = model.train_step(input_ids, batch["labels"],
+                                    lambda out, t: loss_fn(out.view(-1, config.vocab_size).float(), t.view(-1)),
+                                    schedule="1f1b")
+        else:
+            outputs = model(input_ids)
+            labels = batch["labels"].to(bert.head_device)
+            loss = loss_fn(outputs.view(-1, config.vocab_size).float(), labels.view(-1))
+            loss.backward()
         optimizer.step()
         optimizer.zero_grad()
         bert.advance_rng()

@@ -63,3 +63,24 @@ def test_idle_time_table_shape():
     out.float().sum().backward()
     rows = a.tracker.table(1)
     assert rows[0] == ["Device", "Average Idle Time (ms)"] and len(rows) == 3
+
+
+def test_1f1b_schedule_matches_gpipe_with_dropout():
+    """1F1B and fill-drain give the same gradients (same dropout masks per micro-batch)."""
+    cfg = C.BERT_TINY
+    ds = SyntheticLMDataset(cfg, 8, seq_len=32, seed=1)
+    V = cfg.vocab_size
+
+    def loss_fn(out, t):
+        return torch.nn.functional.cross_entropy(out.reshape(-1, V).float(), t.reshape(-1))
+
+    res = []
+    for sched in ("gpipe", "1f1b"):
+        a = BertModelWithMP(cfg, devices=["cpu", "cpu", "cpu"], impl="fused", seed=4)
+        a.train()
+        pipe = a.to_pipeline(chunks=4, checkpoint="never")
+        loss = pipe.train_step(ds.input_ids, ds.labels, loss_fn, schedule=sched)
+        res.append((loss.item(), {n: p.grad.clone() for n, p in a.named_parameters() if p.grad is not None}))
+    assert abs(res[0][0] - res[1][0]) < 1e-6
+    for n in res[0][1]:
+        assert torch.allclose(res[0][1][n], res[1][1][n], atol=1e-6), n
