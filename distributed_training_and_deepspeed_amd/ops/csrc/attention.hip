@@ -191,9 +191,9 @@ struct TileLoader {
 // grid: (ceil(S/128), B*H); block 256 = 4 waves x 32 queries.  KV tiles of 64 keys,
 // double-buffered in LDS with the next tile's global loads issued before the current tile's
 // MFMAs (written to the other buffer afterwards): one barrier per tile.
-template <int D, int OCC>
+template <int D, int OCC, int BN>
 __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
-  constexpr int BN = 64, KP = D + 8, VP = D + 8, NC = D / 16, NDB = D / 32;
+  constexpr int KP = D + 8, VP = D + 8, NC = D / 16, NDB = D / 32, NKB = BN / 32;
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * VP];
 
@@ -237,9 +237,9 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     if (t + 1 < nt) { kl.load(kbase, a.ld, k0 + BN, S); vl.load(vbase, a.ld, k0 + BN, S); }
     const bf16* K = Ks[buf];
     const bf16* V = Vs[buf];
-    f32x16 sacc[2];
+    f32x16 sacc[NKB];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int kb = 0; kb < NKB; ++kb) {
       f32x16 acc = f32x16{};
 #pragma unroll
       for (int c = 0; c < NC; ++c)
@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     float tmax = -INFINITY;
     if (slow) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int key = k0 + kb * 32 + crow(i, hh);
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
         }
     } else {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, sacc[kb][i]);
       tmax *= sc2;
@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     const float msc = slow ? 1.f : sc2;
     float psum = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float pv = fexp2(fmaf(sacc[kb][i], msc, -mexp));
@@ -293,7 +293,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     }
     if (drop) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
+      for (int kb = 0; kb < NKB; ++kb) {
         const int kw = (k0 >> 5) + kb;
         const uint32_t mw = kw < a.W ? mcol[(size_t)kw * S] : 0u;
 #pragma unroll
@@ -302,7 +302,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     }
     // O^T += V^T . P^T: the score accumulator is the B operand; V^T comes from transposed reads
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 pf;
@@ -333,16 +333,28 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
 template <int D>
 __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout,
                                                              float* __restrict__ delta, int B, int S, int H, int ldo) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int row = blockIdx.x;  // b*S + s
-  const int b = row / S, s = row % S;
-  for (int h = w; h < H; h += 4) {
-    float acc = 0.f;
-    const size_t off = (size_t)row * ldo + h * D;
+  // one thread = 8 contiguous elements (16-byte loads); D/8 threads per (row, head) reduce with
+  // xor shuffles.  256 threads cover 256*8/D (row, head) pairs.
+  constexpr int TPH = D / 8;
+  const long long pair = ((long long)blockIdx.x * 256 + threadIdx.x) / TPH;  // (row, head) index
+  const int sub = threadIdx.x % TPH;
+  const long long npairs = (long long)B * S * H;
+  float acc = 0.f;
+  if (pair < npairs) {
+    const int row = (int)(pair / H), h = (int)(pair % H);
+    const size_t off = (size_t)row * ldo + h * D + sub * 8;
+    float x[8], y[8];
+    vload<bf16, 8>(o + off, x);
+    vload<bf16, 8>(dout + off, y);
 #pragma unroll
-    for (int d = lane; d < D; d += 64) acc += (float)o[off + d] * (float)dout[off + d];
-    acc = wave_sum(acc);
-    if (lane == 0) delta[((size_t)b * H + h) * S + s] = acc;
+    for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+  }
+#pragma unroll
+  for (int m = TPH / 2; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if (pair < npairs && sub == 0) {
+    const int row = (int)(pair / H), h = (int)(pair % H);
+    const int b = row / S, sq = row % S;
+    delta[((size_t)b * H + h) * S + sq] = acc;
   }
 }
 
@@ -356,9 +368,9 @@ struct BwdArgs {
 
 // dK, dV: grid (ceil(S/128), B*H); block 256 = 4 waves x 32 keys ("key on the lane").
 // Query tiles of 64 rows (Q, dO row-major in LDS, double-buffered).
-template <int D, int OCC>
+template <int D, int OCC, int BM>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
-  constexpr int BM = 64, QP = D + 8, NC = D / 16, NDB = D / 32;
+  constexpr int QP = D + 8, NC = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * QP];
   __shared__ __attribute__((aligned(16))) bf16 Os[2][BM * QP];
   __shared__ float lse_s[2][BM], del_s[2][BM];
@@ -483,9 +495,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
 // dQ: grid (ceil(S/128), B*H); block 256 = 4 waves x 32 queries (query on the lane, as in the
 // forward); recomputes S^T and dP^T per 64-key tile and accumulates dQ^T = K^T.dS^T in
 // registers -- no atomics, no cross-workgroup reduction.
-template <int D, int OCC>
+template <int D, int OCC, int BN>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
-  constexpr int BN = 64, KP = D + 8, NC = D / 16, NDB = D / 32;
+  constexpr int KP = D + 8, NC = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * KP];
 
@@ -536,7 +548,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
     const bf16* V = Vs[buf];
     const bool needmask = !qvalid || (k0 + BN > S) || (a.causal && k0 + BN - 1 > q0);
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int kb = 0; kb < BN / 32; ++kb) {
       f32x16 sacc = f32x16{}, pacc = f32x16{};
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -605,6 +617,18 @@ static int occupancy(int which) {
   return v[which];
 }
 
+// Keys per K/V tile of the head_dim-64 forward (which=0) and dQ (which=1) kernels: 64 (3 waves
+// per SIMD, 37 KB LDS) or 128 (2 waves per SIMD, 74 KB LDS; half the barriers per key).
+// DTD_ATTN_TILE="f,q" overrides for tuning runs.
+static int tile_keys(int which) {
+  static const int defaults[2] = {64, 64};
+  const char* env = getenv("DTD_ATTN_TILE");
+  if (!env) return defaults[which];
+  int v[2] = {defaults[0], defaults[1]};
+  sscanf(env, "%d,%d", &v[0], &v[1]);
+  return v[which];
+}
+
 // q,k,v,o: bf16 views with row stride ld (q/k/v) / ldo (o); lse: [B,H,S] fp32.
 // masks: [2][B*H*S*W] uint32 (W = ceil(S/32)) written here when p > 0 (read by the backward).
 DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const float* slopes,
@@ -629,11 +653,12 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
   dim3 grid((S + 127) / 128, B * H);
   if (D == 64) {
     const int o = occupancy(0);
-    if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3>), grid, dim3(256), 0, s, a);
-    else if (o == 2) hipLaunchKernelGGL((attn_fwd_kernel<64, 2>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(256), 0, s, a);
+    if (tile_keys(0) == 128) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
+    else if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64>), grid, dim3(256), 0, s, a);
+    else if (o == 2) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
   } else if (D == 128) {
-    hipLaunchKernelGGL((attn_fwd_kernel<128, 1>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<128, 1, 64>), grid, dim3(256), 0, s, a);
   } else {
     return (int)hipErrorInvalidValue;
   }
@@ -667,17 +692,22 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   BwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, (bf16*)dk,
             (bf16*)dv, slopes, mA, mB, B, S, H, ld, ldo, causal, W, scale, p};
   if (D == 64) {
-    hipLaunchKernelGGL(attn_bwd_delta_kernel<64>, dim3(B * S), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
-    if (occupancy(1) >= 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 1>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_bwd_delta_kernel<64>, dim3((unsigned)(((long long)B * S * H * 8 + 255) / 256)), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
+    // query tile of the dK/dV loop: 128 rows halves the barriers / exposed load latency per
+    // query row at 2 blocks per CU (75 KB LDS each); DTD_ATTN_DKDV_BM=64 selects the old tile
+    const int bm = getenv("DTD_ATTN_DKDV_BM") ? atoi(getenv("DTD_ATTN_DKDV_BM")) : 128;
+    if (bm == 128) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
+    else if (occupancy(1) >= 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
     const int o = occupancy(2);
-    if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3>), grid, dim3(256), 0, s, a);
-    else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1>), grid, dim3(256), 0, s, a);
+    if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
+    else if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 64>), grid, dim3(256), 0, s, a);
+    else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL(attn_bwd_delta_kernel<128>, dim3(B * S), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<128, 1>), grid, dim3(256), 0, s, a);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<128, 1>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_bwd_delta_kernel<128>, dim3((unsigned)(((long long)B * S * H * 16 + 255) / 256)), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<128, 1, 64>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<128, 1, 64>), grid, dim3(256), 0, s, a);
   }
   DTD_LAUNCH_CHECK();
 }
