@@ -119,10 +119,12 @@ __global__ void __launch_bounds__(256) attn_mask_kernel(uint32_t* __restrict__ m
     if (q < S && kw < W) {
       const uint64_t base = rowbase + (uint64_t)kw * 32;
       const int nk = min(32, S - kw * 32);
-      if ((base & 1) == 0) {
+      const uint64_t i0 = base >> 1;
+      if ((base & 1) == 0 && (uint32_t)i0 <= 0xFFFFFFF0u) {   // 16 counters, one high word
+        const uint32_t ht = g.hi_term((uint32_t)(i0 >> 32)), lo0 = (uint32_t)i0;
 #pragma unroll 4
         for (int j = 0; j < 32; j += 2) {
-          const uint32_t b = g.bits((base + j) >> 1);
+          const uint32_t b = g.bits_lo(lo0 + (j >> 1), ht);
           word |= (uint32_t)((b & 0xffffu) >= thr) << j;
           word |= (uint32_t)((b >> 16) >= thr) << (j + 1);
         }

@@ -172,11 +172,16 @@ struct DropoutRng {
     k1 = mix32((uint32_t)step * 0x85ebca6bU ^ mix32(stream_id + 0x632be5abU) ^ k0);
   }
   // 32 random bits for 64-bit element index i (one mix32 per pair of dropout decisions:
-  // the attention kernels draw B*H*S*S of them per layer, so the hash is kept short).
+  // the attention kernels draw B*H*S*S of them per layer, so the hash is kept short -- the
+  // counter enters the bijective mix32 finalizer directly, 2 integer multiplies per hash;
+  // v_mul_lo_u32 is a quarter-rate VALU op on CDNA, and it bounds the mask generator).
   __device__ __forceinline__ uint32_t bits(uint64_t i) const {
-    const uint32_t lo = (uint32_t)i, hi = (uint32_t)(i >> 32);
-    return mix32(((lo * 0x9e3779b1U) ^ k0) + ((hi * 0xc2b2ae35U) ^ k1));
+    return mix32(((uint32_t)i ^ k0) + hi_term((uint32_t)(i >> 32)));
   }
+  __device__ __forceinline__ uint32_t hi_term(uint32_t hi) const { return (hi * 0xc2b2ae35U) ^ k1; }
+  // bits() for consecutive counters sharing one precomputed hi_term (the caller guarantees the
+  // high word does not change across the run)
+  __device__ __forceinline__ uint32_t bits_lo(uint32_t lo, uint32_t ht) const { return mix32((lo ^ k0) + ht); }
 };
 // Two keep-decisions per 32 random bits (16-bit thresholds: p quantised to 1/65536).
 __host__ __device__ __forceinline__ uint32_t keep_threshold(float p) {

@@ -63,7 +63,7 @@ def keep_mask(numel: int, p: float, seed: int, step: int, sid: int, device="cpu"
     i = e >> 1
     lo = i & M32
     hi = i >> 32
-    b = _mix32((((lo * 0x9E3779B1) & M32) ^ k0) + (((hi * 0xC2B2AE35) & M32) ^ k1))
+    b = _mix32(((lo ^ k0) + (((hi * 0xC2B2AE35) & M32) ^ k1)) & M32)
     h16 = torch.where((e & 1) == 1, b >> 16, b & 0xFFFF)
     return h16 >= keep_threshold(p)
 
