@@ -6,7 +6,7 @@ RCCL collectives issued by torch, and are captured by ``torch.cuda.graph`` like 
 
 On a machine with a GPU the library is REQUIRED: ``lib()`` raises if it cannot be built or
 loaded (no silent fallback to eager PyTorch on the GPU path).  On CPU-only hosts the pure
-PyTorch reference implementations in ``ops/ref.py`` are used instead.
+PyTorch reference branches of ``ops/functional.py`` are used instead.
 """
 from __future__ import annotations
 

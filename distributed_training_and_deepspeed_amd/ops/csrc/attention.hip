@@ -229,6 +229,16 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   const int kend = a.causal ? min(S, qblk + 128) : S;
   const int nt = (kend + BN - 1) / BN;
   TileLoader<D, BN> kl, vl;
+  // dropout keep words of a key tile (one per 32 keys), prefetched a tile ahead with K/V
+  uint32_t mwc[NKB], mwn[NKB];
+  auto load_words = [&](int k0, uint32_t* out) {
+#pragma unroll
+    for (int j = 0; j < NKB; ++j) {
+      const int kw = (k0 >> 5) + j;
+      out[j] = drop && kw < a.W ? mcol[(size_t)kw * S] : 0u;
+    }
+  };
+  load_words(0, mwc);
   kl.load(kbase, a.ld, 0, S);
   vl.load(vbase, a.ld, 0, S);
   kl.store(Ks[0], KP);
@@ -236,7 +246,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   __syncthreads();
   for (int t = 0; t < nt; ++t) {
     const int buf = t & 1, k0 = t * BN;
-    if (t + 1 < nt) { kl.load(kbase, a.ld, k0 + BN, S); vl.load(vbase, a.ld, k0 + BN, S); }
+    if (t + 1 < nt) { kl.load(kbase, a.ld, k0 + BN, S); vl.load(vbase, a.ld, k0 + BN, S); load_words(k0 + BN, mwn); }
     const bf16* K = Ks[buf];
     const bf16* V = Vs[buf];
     f32x16 sacc[NKB];
@@ -297,7 +307,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
         const int kw = (k0 >> 5) + kb;
-        const uint32_t mw = kw < a.W ? mcol[(size_t)kw * S] : 0u;
+        const uint32_t mw = mwc[kb];
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[kb][i] = keep_bits(sacc[kb][i], mw, crow(i, hh));
       }
@@ -313,7 +323,10 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int d = 0; d < NDB; ++d) oacc[d] = mfma32(tr_operand(V, VP, kb * 32 + 16 * s, d * 32, lane), pf, oacc[d]);
       }
-    if (t + 1 < nt) { kl.store(Ks[buf ^ 1], KP); vl.store(Vs[buf ^ 1], VP); }
+    if (t + 1 < nt) { kl.store(Ks[buf ^ 1], KP); vl.store(Vs[buf ^ 1], VP);
+#pragma unroll
+      for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
+    }
     __syncthreads();
   }
   if (!qvalid) return;
@@ -375,7 +388,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   constexpr int QP = D + 8, NC = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * QP];
   __shared__ __attribute__((aligned(16))) bf16 Os[2][BM * QP];
-  __shared__ float lse_s[2][BM], del_s[2][BM];
+  __shared__ __attribute__((aligned(16))) float lse_s[2][BM], del_s[2][BM];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, r = lane & 31;
   int tx, ty;
@@ -420,19 +433,36 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       del_r = qq < S ? delb[qq] : 0.f;
     }
   };
+  // dropout keep words of a query tile (one per 32 query rows), prefetched a tile ahead with
+  // the Q/dO loads so their global-load latency is never waited on inside the tile
+  constexpr int NQW = BM / 32;
+  uint32_t mwc[NQW], mwn[NQW];
+  auto load_words = [&](int q0, uint32_t* out) {
+#pragma unroll
+    for (int j = 0; j < NQW; ++j) {
+      const int qw = (q0 >> 5) + j;
+      out[j] = drop && qw < a.W ? mcol[(size_t)qw * S] : 0u;
+    }
+  };
   ql.load(qbase, a.ld, qstart, S);
   ol.load(obase, a.ldo, qstart, S);
   load_stats(qstart);
+  load_words(qstart, mwc);
   ql.store(Qs[0], QP);
   ol.store(Os[0], QP);
   if (threadIdx.x < BM) { lse_s[0][threadIdx.x] = lse_r; del_s[0][threadIdx.x] = del_r; }
   __syncthreads();
   for (int t = 0; t < nt; ++t) {
     const int buf = t & 1, q0 = qstart + t * BM;
-    if (t + 1 < nt) { ql.load(qbase, a.ld, q0 + BM, S); ol.load(obase, a.ldo, q0 + BM, S); load_stats(q0 + BM); }
+    if (t + 1 < nt) {
+      ql.load(qbase, a.ld, q0 + BM, S);
+      ol.load(obase, a.ldo, q0 + BM, S);
+      load_stats(q0 + BM);
+      load_words(q0 + BM, mwn);
+    }
     const bf16* Q = Qs[buf];
     const bf16* O = Os[buf];
-#pragma unroll
+#pragma unroll 1
     for (int qb = 0; qb < BM / 32; ++qb) {
       f32x16 sacc = f32x16{}, pacc = f32x16{};
 #pragma unroll
@@ -441,23 +471,38 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
         pacc = mfma32(*reinterpret_cast<const bf16x8*>(&O[(qb * 32 + r) * QP + 16 * c + 8 * hh]), vf[c], pacc);
       }
       const int qrow0 = q0 + qb * 32;
-      const bool needmask = !kvalid || (qrow0 + 32 > S) || (a.causal && key > qrow0);
-      const uint32_t mw = drop && (qrow0 >> 5) < a.W ? mcol[(size_t)(qrow0 >> 5) * S] : 0u;
+      // block-uniform predicate (a scalar branch, never a per-element one)
+      const bool needmask = (kblk + 128 > S) || (qrow0 + 32 > S) || (a.causal && kblk + 127 > qrow0);
+      uint32_t mw = mwc[0];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qr = qb * 32 + crow(i, hh);
-        float pv = fexp2(fmaf(sacc[i], sc2, kbias - lse_s[buf][qr]));
-        if (needmask) {
-          const int qq = q0 + qr;
-          if (!kvalid || qq >= S || (a.causal && key > qq)) pv = 0.f;
+      for (int j = 1; j < NQW; ++j) mw = qb == j ? mwc[j] : mw;   // register select, no scratch
+      // row statistics of this lane's 16 accumulator rows (rows 8g + 4hh + 0..3 are contiguous):
+      // 8 ds_read_b128 issued together instead of 32 dependent scalar LDS reads
+      f32x4 L4[4], D4[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        L4[g] = *reinterpret_cast<const f32x4*>(&lse_s[buf][qb * 32 + 8 * g + 4 * hh]);
+        D4[g] = *reinterpret_cast<const f32x4*>(&del_s[buf][qb * 32 + 8 * g + 4 * hh]);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[i] = fexp2(fmaf(sacc[i], sc2, kbias - L4[i >> 2][i & 3]));  // P
+      if (needmask) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qq = qrow0 + crow(i, hh);
+          const bool ok = kvalid && qq < S && !(a.causal && key > qq);
+          sacc[i] = ok ? sacc[i] : 0.f;
         }
-        if (drop) {
-          sacc[i] = keep_bits(pv, mw, crow(i, hh));           // dropped P (x 1/(1-p) at the end)
-          pacc[i] = pv * fmaf(keep_bits(pacc[i], mw, crow(i, hh)), inv_keep, -del_s[buf][qr]);  // dS
-        } else {
-          sacc[i] = pv;
-          pacc[i] = pv * (pacc[i] - del_s[buf][qr]);
+      }
+      if (drop) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          pacc[i] = sacc[i] * fmaf(keep_bits(pacc[i], mw, crow(i, hh)), inv_keep, -D4[i >> 2][i & 3]);  // dS
+          sacc[i] = keep_bits(sacc[i], mw, crow(i, hh));                                          // P*mask (dV)
         }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) pacc[i] = sacc[i] * (pacc[i] - D4[i >> 2][i & 3]);
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -475,6 +520,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       ql.store(Qs[buf ^ 1], QP);
       ol.store(Os[buf ^ 1], QP);
       if (threadIdx.x < BM) { lse_s[buf ^ 1][threadIdx.x] = lse_r; del_s[buf ^ 1][threadIdx.x] = del_r; }
+#pragma unroll
+      for (int j = 0; j < NQW; ++j) mwc[j] = mwn[j];
     }
     __syncthreads();
   }
@@ -538,6 +585,16 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   const int kend = a.causal ? min(S, qblk + 128) : S;
   const int nt = (kend + BN - 1) / BN;
   TileLoader<D, BN> kl, vl;
+  // dropout keep words of a key tile (one per 32 keys), prefetched a tile ahead with K/V
+  uint32_t mwc[BN / 32], mwn[BN / 32];
+  auto load_words = [&](int k0, uint32_t* out) {
+#pragma unroll
+    for (int j = 0; j < BN / 32; ++j) {
+      const int kw = (k0 >> 5) + j;
+      out[j] = drop && kw < a.W ? mcol[(size_t)kw * S] : 0u;
+    }
+  };
+  load_words(0, mwc);
   kl.load(kbase, a.ld, 0, S);
   vl.load(vbase, a.ld, 0, S);
   kl.store(Ks[0], KP);
@@ -545,7 +602,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   __syncthreads();
   for (int t = 0; t < nt; ++t) {
     const int buf = t & 1, k0 = t * BN;
-    if (t + 1 < nt) { kl.load(kbase, a.ld, k0 + BN, S); vl.load(vbase, a.ld, k0 + BN, S); }
+    if (t + 1 < nt) { kl.load(kbase, a.ld, k0 + BN, S); vl.load(vbase, a.ld, k0 + BN, S); load_words(k0 + BN, mwn); }
     const bf16* K = Ks[buf];
     const bf16* V = Vs[buf];
     const bool needmask = !qvalid || (k0 + BN > S) || (a.causal && k0 + BN - 1 > q0);
@@ -558,7 +615,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
         pacc = mfma32(*reinterpret_cast<const bf16x8*>(&V[(kb * 32 + r) * KP + 16 * c + 8 * hh]), of[c], pacc);
       }
       const int kw = (k0 >> 5) + kb;
-      const uint32_t mw = drop && kw < a.W ? mcol[(size_t)kw * S] : 0u;
+      const uint32_t mw = mwc[kb];
       // P = exp2(s*log2e - lse): 2 VALU on interior tiles without ALiBi
       if (needmask || sl2 != 0.f) {
 #pragma unroll
@@ -589,7 +646,10 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
         for (int d = 0; d < NDB; ++d) dq[d] = mfma32(tr_operand(K, KP, kb * 32 + 16 * s, d * 32, lane), sb, dq[d]);
       }
     }
-    if (t + 1 < nt) { kl.store(Ks[buf ^ 1], KP); vl.store(Vs[buf ^ 1], KP); }
+    if (t + 1 < nt) { kl.store(Ks[buf ^ 1], KP); vl.store(Vs[buf ^ 1], KP);
+#pragma unroll
+      for (int j = 0; j < BN / 32; ++j) mwc[j] = mwn[j];
+    }
     __syncthreads();
   }
   if (!qvalid) return;

@@ -1,9 +1,9 @@
 """Functional front-end of the fused ops.
 
 Each function runs the gfx950 HIP kernel for CUDA(HIP) tensors and the PyTorch reference
-(``ops/ref.py`` semantics, same dropout masks) for CPU tensors.  Parameter-gradient outputs
+(same semantics and dropout masks as the kernels) for CPU tensors.  Parameter-gradient outputs
 are written into caller-provided destination tensors (``main_grad`` views of the flat
-gradient buffers, see ``parallel/grad_buffer.py``) with overwrite-or-accumulate semantics,
+gradient buffers, see ``parallel/flat.py``) with overwrite-or-accumulate semantics,
 which is how the framework avoids a separate gradient-accumulation pass.
 """
 from __future__ import annotations

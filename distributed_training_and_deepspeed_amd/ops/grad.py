@@ -4,7 +4,7 @@ The fused modules' backward passes write weight/bias gradients straight into the
 storage instead of returning them to autograd:
 
 * if the parameter has ``main_grad`` (a view into a flat gradient buffer owned by the DDP /
-  ZeRO engine, ``parallel/grad_buffer.py``), the wgrad GEMM writes into that view with
+  ZeRO engine, ``parallel/flat.py``), the wgrad GEMM writes into that view with
   beta = 0 on the first contribution of the step and beta = 1 afterwards (tied weights,
   gradient accumulation) -- no AccumulateGrad copy, no separate bucket-flatten pass;
 * otherwise the gradient lands in ``param.grad`` (created on first use), so any stock
