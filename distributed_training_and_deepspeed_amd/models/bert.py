@@ -18,7 +18,7 @@ from torch import nn
 
 from .config import BERT_BASE, TransformerConfig, get_config
 from .layers import Embeddings, MLMHead
-from .transformer import Runtime, TransformerLayer
+from .transformer import Runtime, TransformerLayer, prefetch_masks
 
 
 @dataclass
@@ -49,6 +49,8 @@ class BertForMaskedLM(nn.Module):
         return [self.embeddings.word] if self.head.decoder_w is None else []
 
     def encode(self, input_ids: torch.Tensor) -> torch.Tensor:
+        if input_ids.is_cuda and self.training:
+            prefetch_masks(self.layers, input_ids)
         x = self.embeddings(input_ids)
         for layer in self.layers:
             x = layer(x)

@@ -19,7 +19,7 @@ from torch import nn
 
 from .config import BLOOM_560M, TransformerConfig, get_config
 from .layers import Embeddings, LayerNorm, LMHead
-from .transformer import Runtime, TransformerLayer
+from .transformer import Runtime, TransformerLayer, prefetch_masks
 
 
 @dataclass
@@ -51,6 +51,8 @@ class CausalLM(nn.Module):
         return [self.embeddings.word]
 
     def encode(self, input_ids: torch.Tensor) -> torch.Tensor:
+        if input_ids.is_cuda and self.training:
+            prefetch_masks(self.layers, input_ids)
         x = self.embeddings(input_ids)
         for layer in self.layers:
             x = layer(x)

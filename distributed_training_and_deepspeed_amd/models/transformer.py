@@ -65,6 +65,14 @@ class Runtime:
         return x.is_cuda
 
 
+def prefetch_masks(layers, input_ids: torch.Tensor) -> None:
+    """Issue every layer's attention-dropout mask generation (fused bf16 path only)."""
+    B, S = input_ids.shape[0], input_ids.shape[1]
+    for layer in layers:
+        if layer.rt.use_fused(input_ids) and layer.qkv_w.dtype == torch.bfloat16:
+            layer.prefetch_attention_masks(B, S, input_ids.device)
+
+
 def ref_dropout(x, p, training, rt: Runtime, sid):
     if not training or p <= 0:
         return x
@@ -78,6 +86,7 @@ class TransformerLayer(nn.Module):
         super().__init__()
         h, f = cfg.hidden_size, cfg.ffn_size
         self.cfg, self.rt = cfg, rt
+        self._prefetched = None  # (sid, B, S, PendingMasks) from prefetch_attention_masks
         self.qkv_w = nn.Parameter(torch.empty(3 * h, h))
         self.qkv_b = nn.Parameter(torch.zeros(3 * h))
         self.o_w = nn.Parameter(torch.empty(h, h))
@@ -110,6 +119,20 @@ class TransformerLayer(nn.Module):
     def params(self):
         return (self.qkv_w, self.qkv_b, self.o_w, self.o_b, self.ln1_g, self.ln1_b,
                 self.fc1_w, self.fc1_b, self.fc2_w, self.fc2_b, self.ln2_g, self.ln2_b)
+
+    def prefetch_attention_masks(self, B: int, S: int, device) -> None:
+        """Start generating this layer's attention-dropout keep bits now, on the side stream.
+        The masks depend only on (seed, step, call site), not on activations, so a model issues
+        every layer's generation at the start of its forward and the VALU-only hash work runs
+        under the whole forward's GEMMs instead of in front of each attention.  The masks are
+        kept for the backward anyway, so this costs no extra peak memory."""
+        c = self.cfg
+        if not (self.training and c.attn_dropout > 0 and torch.is_grad_enabled()):
+            return
+        sid = self.rt.rng.sid(self.sid_attn)
+        pend = A.attn_masks_async(B, S, c.num_heads, c.head_dim, c.attn_dropout, self.rt.rng, sid, device)
+        if pend is not None:
+            self._prefetched = (sid, B, S, pend)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x: [B, S, h] -> [B, S, h]"""
@@ -173,9 +196,14 @@ class _FusedLayerFn(torch.autograd.Function):
         sa, s1, s2 = rng.sid(layer.sid_attn), rng.sid(layer.sid_1), rng.sid(layer.sid_2)
         x2d = x.reshape(T, h)
         eps = c.ln_eps
-        # attention-dropout keep bits: generated on a side stream, overlapping the QKV GEMM
-        pend = A.attn_masks_async(B, S, H, D, p_a, rng, sa, x.device) \
-            if x.is_cuda and x.dtype == torch.bfloat16 else None
+        # attention-dropout keep bits: generated on a side stream -- prefetched by the model at
+        # the start of its forward, else issued here to overlap at least the QKV GEMM
+        pre, layer._prefetched = layer._prefetched, None
+        if pre is not None and pre[:3] == (sa, B, S) and p_a > 0:
+            pend = pre[3]
+        else:
+            pend = A.attn_masks_async(B, S, H, D, p_a, rng, sa, x.device) \
+                if x.is_cuda and x.dtype == torch.bfloat16 else None
         if c.pre_ln:
             _, a_in, m1, r1 = Fx.ln_fwd(None, x2d, g1, b1, eps, 0.0, rng, 0)
         else:
