@@ -31,6 +31,7 @@
 // (bounds-masked), head_dim 64 or 128.  q/k/v/o are strided views (row stride `ld`) into the
 // fused [B*S, 3*H*D] projection output, so no transpose/copy kernels are needed.
 #include <stdio.h>
+#include <type_traits>
 #include <stdlib.h>
 
 #include "common.h"
@@ -172,27 +173,31 @@ struct TileLoader {
   static constexpr int CH = ROWS * D / 8;  // 16-byte chunks
   static constexpr int PER = (CH + 255) / 256;
   bf16x8 reg[PER];
+  static_assert(CH % 256 == 0, "tile must split evenly over 256 threads");
+  // Branch-free: rows past the end are loaded from the last valid row and zeroed by a select, so
+  // the loads form straight-line code and the compiler can count them (partial vmcnt waits)
+  // while a second tile's loads are still in flight (the register ring of the kernels below).
   __device__ __forceinline__ void load(const bf16* base, int ld, int row0, int nrows) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + 256 * i;
       const int rr = c / (D / 8), dc = (c % (D / 8)) * 8;
-      reg[i] = bf16x8{};
-      if (c < CH && row0 + rr < nrows) reg[i] = *reinterpret_cast<const bf16x8*>(base + (size_t)(row0 + rr) * ld + dc);
+      const int row = min(row0 + rr, nrows - 1);
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(base + (size_t)row * ld + dc);
+      reg[i] = (row0 + rr < nrows) ? v : bf16x8{};
     }
   }
   __device__ __forceinline__ void store(bf16* lds, int stride) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + 256 * i;
-      if (c < CH) *reinterpret_cast<bf16x8*>(lds + (c / (D / 8)) * stride + (c % (D / 8)) * 8) = reg[i];
+      *reinterpret_cast<bf16x8*>(lds + (c / (D / 8)) * stride + (c % (D / 8)) * 8) = reg[i];
     }
   }
 };
 
-// grid: (ceil(S/128), B*H); block 256 = 4 waves x 32 queries.  KV tiles of 64 keys,
-// double-buffered in LDS with the next tile's global loads issued before the current tile's
-// MFMAs (written to the other buffer afterwards): one barrier per tile.
+// grid: (ceil(S/128), B*H); block 256 = 4 waves x 32 queries.  KV tiles of BN keys,
+// double-buffered in LDS, fed by a 2-deep register ring of global loads: one barrier per tile.
 template <int D, int OCC, int BN>
 __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   constexpr int KP = D + 8, VP = D + 8, NC = D / 16, NDB = D / 32, NKB = BN / 32;
@@ -228,25 +233,40 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
 
   const int kend = a.causal ? min(S, qblk + 128) : S;
   const int nt = (kend + BN - 1) / BN;
-  TileLoader<D, BN> kl, vl;
-  // dropout keep words of a key tile (one per 32 keys), prefetched a tile ahead with K/V
-  uint32_t mwc[NKB], mwn[NKB];
+  // K/V tiles stream through a 2-deep register ring: tile t+2's global loads are issued while
+  // tile t is computed and written to LDS only at the end of tile t+1, so each load has two
+  // tiles of compute to arrive (one tile of MFMA/softmax work is shorter than an HBM round trip).
+  // The dropout keep words (one per 32 keys) ride along in the same ring.
+  TileLoader<D, BN> kl0, vl0, kl1, vl1;
+  uint32_t mwc[NKB], mw0[NKB], mw1[NKB];
+  // unconditional word loads (a valid dummy address without dropout) keep the ring branch-free
+  const uint32_t* wbase = drop ? mcol : reinterpret_cast<const uint32_t*>(a.lse);
+  const size_t wstride = drop ? (size_t)S : 0;
   auto load_words = [&](int k0, uint32_t* out) {
 #pragma unroll
     for (int j = 0; j < NKB; ++j) {
-      const int kw = (k0 >> 5) + j;
-      out[j] = drop && kw < a.W ? mcol[(size_t)kw * S] : 0u;
+      const int kw = min((k0 >> 5) + j, a.W - 1);
+      out[j] = wbase[(size_t)kw * wstride];
     }
   };
   load_words(0, mwc);
-  kl.load(kbase, a.ld, 0, S);
-  vl.load(vbase, a.ld, 0, S);
-  kl.store(Ks[0], KP);
-  vl.store(Vs[0], VP);
+  kl0.load(kbase, a.ld, 0, S);
+  vl0.load(vbase, a.ld, 0, S);
+  kl0.store(Ks[0], KP);
+  vl0.store(Vs[0], VP);
+  {
+    const int k1 = min(1, nt - 1) * BN, k2 = min(2, nt - 1) * BN;
+    kl1.load(kbase, a.ld, k1, S); vl1.load(vbase, a.ld, k1, S); load_words(k1, mw1);
+    kl0.load(kbase, a.ld, k2, S); vl0.load(vbase, a.ld, k2, S); load_words(k2, mw0);
+  }
   __syncthreads();
-  for (int t = 0; t < nt; ++t) {
+  // SET = register set holding tile t+1 (t even -> 1, t odd -> 0)
+  auto tile = [&](auto set_c, int t) {
+    constexpr int SET = decltype(set_c)::value;
+    TileLoader<D, BN>& kn = SET ? kl1 : kl0;
+    TileLoader<D, BN>& vn = SET ? vl1 : vl0;
+    uint32_t* mwn = SET ? mw1 : mw0;
     const int buf = t & 1, k0 = t * BN;
-    if (t + 1 < nt) { kl.load(kbase, a.ld, k0 + BN, S); vl.load(vbase, a.ld, k0 + BN, S); load_words(k0 + BN, mwn); }
     const bf16* K = Ks[buf];
     const bf16* V = Vs[buf];
     f32x16 sacc[NKB];
@@ -306,7 +326,6 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     if (drop) {
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
-        const int kw = (k0 >> 5) + kb;
         const uint32_t mw = mwc[kb];
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[kb][i] = keep_bits(sacc[kb][i], mw, crow(i, hh));
@@ -323,11 +342,22 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int d = 0; d < NDB; ++d) oacc[d] = mfma32(tr_operand(V, VP, kb * 32 + 16 * s, d * 32, lane), pf, oacc[d]);
       }
-    if (t + 1 < nt) { kl.store(Ks[buf ^ 1], KP); vl.store(Vs[buf ^ 1], VP);
+    if (t + 1 < nt) {
+      kn.store(Ks[buf ^ 1], KP);
+      vn.store(Vs[buf ^ 1], VP);
 #pragma unroll
       for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
+      // tile t+3 (clamped to the last tile: a harmless reload keeps the issue unconditional)
+      const int kf = min(t + 3, nt - 1) * BN;
+      kn.load(kbase, a.ld, kf, S);
+      vn.load(vbase, a.ld, kf, S);
+      load_words(kf, mwn);
     }
     __syncthreads();
+  };
+  for (int t = 0; t < nt; t += 2) {
+    tile(std::integral_constant<int, 1>{}, t);
+    if (t + 1 < nt) tile(std::integral_constant<int, 0>{}, t + 1);
   }
   if (!qvalid) return;
   const float inv_l = l > 0.f ? inv_keep / l : 0.f;   // dropout 1/(1-p) folded in here
@@ -584,25 +614,37 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
 
   const int kend = a.causal ? min(S, qblk + 128) : S;
   const int nt = (kend + BN - 1) / BN;
-  TileLoader<D, BN> kl, vl;
-  // dropout keep words of a key tile (one per 32 keys), prefetched a tile ahead with K/V
-  uint32_t mwc[BN / 32], mwn[BN / 32];
+  // K/V tiles + dropout keep words through a 2-deep register ring (see attn_fwd_kernel)
+  constexpr int NKB = BN / 32;
+  TileLoader<D, BN> kl0, vl0, kl1, vl1;
+  uint32_t mwc[NKB], mw0[NKB], mw1[NKB];
+  // unconditional word loads (a valid dummy address without dropout) keep the ring branch-free
+  const uint32_t* wbase = drop ? mcol : reinterpret_cast<const uint32_t*>(a.lse);
+  const size_t wstride = drop ? (size_t)S : 0;
   auto load_words = [&](int k0, uint32_t* out) {
 #pragma unroll
-    for (int j = 0; j < BN / 32; ++j) {
-      const int kw = (k0 >> 5) + j;
-      out[j] = drop && kw < a.W ? mcol[(size_t)kw * S] : 0u;
+    for (int j = 0; j < NKB; ++j) {
+      const int kw = min((k0 >> 5) + j, a.W - 1);
+      out[j] = wbase[(size_t)kw * wstride];
     }
   };
   load_words(0, mwc);
-  kl.load(kbase, a.ld, 0, S);
-  vl.load(vbase, a.ld, 0, S);
-  kl.store(Ks[0], KP);
-  vl.store(Vs[0], KP);
+  kl0.load(kbase, a.ld, 0, S);
+  vl0.load(vbase, a.ld, 0, S);
+  kl0.store(Ks[0], KP);
+  vl0.store(Vs[0], KP);
+  {
+    const int k1 = min(1, nt - 1) * BN, k2 = min(2, nt - 1) * BN;
+    kl1.load(kbase, a.ld, k1, S); vl1.load(vbase, a.ld, k1, S); load_words(k1, mw1);
+    kl0.load(kbase, a.ld, k2, S); vl0.load(vbase, a.ld, k2, S); load_words(k2, mw0);
+  }
   __syncthreads();
-  for (int t = 0; t < nt; ++t) {
+  auto tile = [&](auto set_c, int t) {
+    constexpr int SET = decltype(set_c)::value;
+    TileLoader<D, BN>& kn = SET ? kl1 : kl0;
+    TileLoader<D, BN>& vn = SET ? vl1 : vl0;
+    uint32_t* mwn = SET ? mw1 : mw0;
     const int buf = t & 1, k0 = t * BN;
-    if (t + 1 < nt) { kl.load(kbase, a.ld, k0 + BN, S); vl.load(vbase, a.ld, k0 + BN, S); load_words(k0 + BN, mwn); }
     const bf16* K = Ks[buf];
     const bf16* V = Vs[buf];
     const bool needmask = !qvalid || (k0 + BN > S) || (a.causal && k0 + BN - 1 > q0);
@@ -614,7 +656,6 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
         sacc = mfma32(*reinterpret_cast<const bf16x8*>(&K[(kb * 32 + r) * KP + 16 * c + 8 * hh]), qf[c], sacc);
         pacc = mfma32(*reinterpret_cast<const bf16x8*>(&V[(kb * 32 + r) * KP + 16 * c + 8 * hh]), of[c], pacc);
       }
-      const int kw = (k0 >> 5) + kb;
       const uint32_t mw = mwc[kb];
       // P = exp2(s*log2e - lse): 2 VALU on interior tiles without ALiBi
       if (needmask || sl2 != 0.f) {
@@ -646,11 +687,22 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
         for (int d = 0; d < NDB; ++d) dq[d] = mfma32(tr_operand(K, KP, kb * 32 + 16 * s, d * 32, lane), sb, dq[d]);
       }
     }
-    if (t + 1 < nt) { kl.store(Ks[buf ^ 1], KP); vl.store(Vs[buf ^ 1], KP);
+    if (t + 1 < nt) {
+      kn.store(Ks[buf ^ 1], KP);
+      vn.store(Vs[buf ^ 1], KP);
 #pragma unroll
-      for (int j = 0; j < BN / 32; ++j) mwc[j] = mwn[j];
+      for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
+      // tile t+3 (clamped to the last tile: a harmless reload keeps the issue unconditional)
+      const int kf = min(t + 3, nt - 1) * BN;
+      kn.load(kbase, a.ld, kf, S);
+      vn.load(vbase, a.ld, kf, S);
+      load_words(kf, mwn);
     }
     __syncthreads();
+  };
+  for (int t = 0; t < nt; t += 2) {
+    tile(std::integral_constant<int, 1>{}, t);
+    if (t + 1 < nt) tile(std::integral_constant<int, 0>{}, t + 1);
   }
   if (!qvalid) return;
   bf16* qp = a.dq + (size_t)(b * S + q) * a.ld + h * D;
@@ -671,7 +723,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
 // fwd, dK/dV, dQ.  Defaults are the measured best on MI355X (scripts/bench_attn.py); override
 // with DTD_ATTN_OCC="f,kv,q" for tuning runs.
 static int occupancy(int which) {
-  static const int defaults[3] = {3, 2, 3};
+  static const int defaults[3] = {2, 2, 2};
   const char* env = getenv("DTD_ATTN_OCC");
   if (!env) return defaults[which];
   int v[3] = {defaults[0], defaults[1], defaults[2]};
