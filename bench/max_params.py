@@ -51,7 +51,7 @@ def largest(world: int, stage: int, fraction: float, seq_len: int = 512, batch: 
     cap = MI355X_HBM_BYTES * fraction
     for L, h in candidates():
         pr = project_training_memory(L, h, h // 128, batch, seq_len, precision="bf16", zero_stage=stage,
-                                     world_size=world, extra_params=embed_params(h))
+                                     world_size=world, extra_params=embed_params(h), keep_ffn_act=False)
         # + the logits of one micro-batch (bf16 + fp32 LSE path) and one gathered ZeRO-3 unit
         extra = batch * seq_len * VOCAB * 2 * 2 + (12 * h * h * 2 if stage == 3 else 0)
         if pr.total + extra <= cap and (best is None or pr.params > best[2].params):
@@ -92,7 +92,9 @@ def measure(a) -> dict:
     torch.manual_seed(0)
     t0 = time.time()
     with torch.device(dev):                       # allocate + initialise directly in HBM
-        model = CausalLM(cfg, rt=Runtime(impl="fused", rng=RngState(seed=0, device=dev)))
+        rt = Runtime(impl="fused", rng=RngState(seed=0, device=dev))
+        rt.keep_ffn_act = False                   # memory-bound run: recompute act(u) in backward
+        model = CausalLM(cfg, rt=rt)
     model = model.to(torch.bfloat16)
     n = sum(p.numel() for p in model.parameters())
     conf = {"optimizer": {"type": "Adam", "params": {"lr": 1e-4}},
@@ -117,7 +119,7 @@ def measure(a) -> dict:
     dt = time.perf_counter() - t1
     peak = torch.cuda.max_memory_allocated()
     pr = project_training_memory(L, h, h // 128, 1, a.seq_len, precision="bf16", zero_stage=a.stage,
-                                 world_size=world, extra_params=embed_params(h))
+                                 world_size=world, extra_params=embed_params(h), keep_ffn_act=False)
     res = {"metric": "max trainable params (ZeRO, one training step measured)", "params": n,
            "params_B": round(n / 1e9, 3), "layers": L, "hidden": h, "stage": a.stage, "world": world,
            "peak_alloc_GB": round(peak / 1e9, 1), "projected_GB": round(pr.total / 1e9, 1),

@@ -119,7 +119,7 @@ class MemoryProjection:
 def project_training_memory(layers: int, hidden_size: int, num_heads: int, batch_size: int, seq_len: int,
                             ffn_size: int | None = None, precision: str = "bf16", flash_attention: bool = True,
                             zero_stage: int = 0, world_size: int = 1, capacity: float = MI355X_HBM_BYTES,
-                            extra_params: int = 0) -> MemoryProjection:
+                            extra_params: int = 0, keep_ffn_act: bool = True) -> MemoryProjection:
     """Per-GPU bytes for one training replica on MI355X.
 
     precision 'fp32': fp32 weights + grads + Adam moments (the reference's setting).
@@ -128,7 +128,9 @@ def project_training_memory(layers: int, hidden_size: int, num_heads: int, batch
     fp32 eager: h*(67 + 9*a*s/h)  (reference formula);
     bf16 + flash attention (this framework's fused layer): the tensors it saves --
     layer input, qkv, context, two LN sums (2 B/elt), FFN pre-activation (ffn wide) and
-    fp32 row statistics; dropout masks are regenerated, scores are never stored.
+    fp32 row statistics, plus the FFN activation itself when ``keep_ffn_act`` (the fused
+    layer's default, ``Runtime.keep_ffn_act``); dropout masks are regenerated, scores are
+    never stored.
     """
     h, a, s, b = hidden_size, num_heads, seq_len, batch_size
     ffn = 4 * h if ffn_size is None else ffn_size
@@ -140,6 +142,8 @@ def project_training_memory(layers: int, hidden_size: int, num_heads: int, batch
         w, g, o = 2.0 * n, 2.0 * n, 12.0 * n
         if flash_attention:
             act_per_tok = 2 * (h + 3 * h + h + h + h + ffn) + 4 * 6 + 4 * a  # saved bf16 tensors + stats/LSE
+            if keep_ffn_act:
+                act_per_tok += 2 * ffn
         else:
             act_per_tok = h * (34 + 5 * a * s / h)  # Korthikanti 16-bit form
     N = max(1, world_size)

@@ -49,6 +49,12 @@ class Runtime:
         # no host sync).  None -> exact-size gather (nonzero).  See MLMHead.loss.
         self.mlm_capacity: int | None = None
         self.mlm_overflow: torch.Tensor | None = None   # device flag: a batch exceeded the capacity
+        # Keep the FFN activation act(u) from the forward for the backward (fc2 weight-gradient
+        # input) instead of recomputing it in the activation-backward pass.  Costs one T x ffn
+        # tensor per layer (4.8 GB for BERT-base at 128 x 512 tokens, ~2 % of 288 GB) and saves
+        # its rewrite: the backward pass then moves 3 instead of 4 T x ffn tensors through HBM.
+        # Memory-bound runs (max-params ZeRO-3) turn it off.
+        self.keep_ffn_act = True
 
     def new_sid(self) -> int:
         """Dropout stream id for one call site; deterministic per model structure so two
@@ -223,10 +229,11 @@ class _FusedLayerFn(torch.autograd.Function):
             z2 = m3 = r3 = None
         else:
             z2, out, m3, r3 = Fx.ln_fwd(y, f_in, g2, b2, eps, p_h, rng, s2)
+        a_keep = a if rt.keep_ffn_act else None
         if c.pre_ln:
-            ctx.save_for_backward(x2d, a_in, qkv, actx, lse, z1, f_in, u, m1, r1, m2, r2)
+            ctx.save_for_backward(x2d, a_in, qkv, actx, lse, z1, f_in, u, m1, r1, m2, r2, a_keep)
         else:
-            ctx.save_for_backward(x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3)
+            ctx.save_for_backward(x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3, a_keep)
         ctx.layer = layer
         ctx.amask = amask  # attention dropout keep bits (kernel path) for the backward
         ctx.rng = rng  # the RngState of this forward's device (pipeline stages differ)
@@ -242,22 +249,25 @@ class _FusedLayerFn(torch.autograd.Function):
         (qkv_w, qkv_b, o_w, o_b, g1, b1, w1, bf1, w2, bf2, g2, b2) = layer.params()
         dout = dout.reshape(T, h).contiguous()
         if c.pre_ln:
-            x2d, a_in, qkv, actx, lse, z1, f_in, u, m1, r1, m2, r2 = ctx.saved_tensors
+            x2d, a_in, qkv, actx, lse, z1, f_in, u, m1, r1, m2, r2, a = ctx.saved_tensors
             # out = z1 + dropout(y)
             dy = Fx.dropout(dout, p_h, rng, s2)
             Fx.bias_grad(dy, *_pair(bf2))
             grad_done(bf2)
         else:
-            x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3 = ctx.saved_tensors
+            x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3, a = ctx.saved_tensors
             # out = LN2(f_in + dropout(y)); dz2 = d(out)/d(z2), flows to f_in (residual) and y
             dz2, dy = Fx.ln_bwd(dout, None, z2, m3, r3, g2, p_h, rng, s2, want_dz=True, want_dy=True,
                                 dgamma=_acc(g2), dbeta=_acc(b2), dbias=_acc(bf2))
             for p in (g2, b2, bf2):
                 grad_done(p)
-        # dgrad first: the activation a = act(u) (fc2's wgrad input) is then recomputed inside the
-        # activation-backward pass instead of a separate act_fwd read/write of the T x 4h tensor
+        # dgrad first; without a kept forward activation, a = act(u) (fc2's wgrad input) is
+        # recomputed inside the activation-backward pass (no separate act_fwd read/write)
         da = dy @ w2
-        du, a = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1), want_act=True)
+        if a is None:
+            du, a = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1), want_act=True)
+        else:
+            du = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1))
         grad_done(bf1)
         emit_wgrad(w2, dy, a)
         del a
