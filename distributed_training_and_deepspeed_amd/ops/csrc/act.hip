@@ -15,47 +15,80 @@ namespace {
 
 enum Act : int { kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3 };
 
-__device__ __forceinline__ float act_f(int act, float x) {
-  switch (act) {
-    case kGeluErf: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
-    case kGeluTanh: {
-      const float k = 0.7978845608028654f;
-      return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
-    }
-    case kRelu: return x > 0.f ? x : 0.f;
-    default: return x;
+// Standard-normal CDF Phi(x) = 0.5 (1 + erf(x / sqrt 2)) from one exponential: Abramowitz &
+// Stegun 7.1.26 (|erf error| <= 1.5e-7, far below the bf16 rounding of the outputs) with
+// e = exp(-x^2 / 2), which is also the Gaussian density the GELU derivative needs -- one v_exp,
+// one v_rcp and a handful of FMAs instead of the libm erff's branches and polynomials (the
+// GELU passes are VALU-, not HBM-bound with the libm form).
+__device__ __forceinline__ float phi_cdf(float x, float e) {
+  const float a = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  const float poly = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
+                              0.254829592f);
+  const float erfa = 1.f - poly * e;                  // erf(|x| / sqrt 2)
+  return 0.5f + 0.5f * copysignf(erfa, x);
+}
+__device__ __forceinline__ float gauss_e(float x) { return __expf(-0.5f * x * x); }
+// tanh(y) = 1 - 2 / (1 + e^{2y}): one v_exp + one v_rcp; saturates correctly at +-inf.
+__device__ __forceinline__ float fast_tanh(float y) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * y));
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float x) {
+  if constexpr (ACT == kGeluErf) {
+    return x * phi_cdf(x, gauss_e(x));
+  } else if constexpr (ACT == kGeluTanh) {
+    const float k = 0.7978845608028654f;
+    return 0.5f * x * (1.f + fast_tanh(k * fmaf(0.044715f * x, x * x, x)));
+  } else if constexpr (ACT == kRelu) {
+    return x > 0.f ? x : 0.f;
+  } else {
+    return x;
   }
 }
-__device__ __forceinline__ float act_df(int act, float x) {
-  switch (act) {
-    case kGeluErf: {
-      const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-      const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-      return cdf + x * pdf;
-    }
-    case kGeluTanh: {
-      const float k = 0.7978845608028654f;
-      const float t = tanhf(k * (x + 0.044715f * x * x * x));
-      return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
-    }
-    case kRelu: return x > 0.f ? 1.f : 0.f;
-    default: return 1.f;
+template <int ACT>
+__device__ __forceinline__ float act_df(float x) {
+  if constexpr (ACT == kGeluErf) {
+    const float e = gauss_e(x);
+    return fmaf(x * 0.3989422804014327f, e, phi_cdf(x, e));
+  } else if constexpr (ACT == kGeluTanh) {
+    const float k = 0.7978845608028654f;
+    const float t = fast_tanh(k * fmaf(0.044715f * x, x * x, x));
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+  } else if constexpr (ACT == kRelu) {
+    return x > 0.f ? 1.f : 0.f;
+  } else {
+    return 1.f;
+  }
+}
+// act(x) and act'(x) together (the backward recompute path shares the exponential)
+template <int ACT>
+__device__ __forceinline__ void act_fdf(float x, float& y, float& dy) {
+  if constexpr (ACT == kGeluErf) {
+    const float e = gauss_e(x);
+    const float c = phi_cdf(x, e);
+    y = x * c;
+    dy = fmaf(x * 0.3989422804014327f, e, c);
+  } else {
+    y = act_f<ACT>(x);
+    dy = act_df<ACT>(x);
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ u, T* __restrict__ y, size_t n, int act) {
+template <typename T, int ACT>
+__global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ u, T* __restrict__ y, size_t n) {
   const size_t nv = n / 8;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
     float t[8];
     vload<T, 8>(u + i * 8, t);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = act_f(act, t[j]);
+    for (int j = 0; j < 8; ++j) t[j] = act_f<ACT>(t[j]);
     vstore<T, 8>(y + i * 8, t);
   }
   // tail (n % 8) handled by block 0
   if (blockIdx.x == 0) {
-    for (size_t i = nv * 8 + threadIdx.x; i < n; i += blockDim.x) y[i] = (T)act_f(act, (float)u[i]);
+    for (size_t i = nv * 8 + threadIdx.x; i < n; i += blockDim.x) y[i] = (T)act_f<ACT>((float)u[i]);
   }
 }
 
@@ -65,10 +98,11 @@ __global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ u, T
 // grid = (ceil(cols / (64*VEC)), G); block = 4 waves sharing one 64*VEC-column tile; each wave
 // strides over rows with 4 rows in flight (ILP), and the 4 waves' column sums are combined
 // through LDS into one partial row per block row-group.
-template <typename T, int VEC>
+template <typename T, int VEC, int ACT>
 __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ u,
                                                       T* __restrict__ du, float* __restrict__ part,
-                                                      T* __restrict__ yout, int rows, int cols, int act) {
+                                                      T* __restrict__ yout, int rows, int cols) {
+  constexpr bool kAct = ACT != kNone;
   __shared__ float sh[4][64 * VEC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = (blockIdx.x * 64 + lane) * VEC;
@@ -85,19 +119,22 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, 
       for (int k = 0; k < 4; ++k) {
         const size_t off = (size_t)(r + k * stride) * cols + col;
         vload<T, VEC>(dy + off, d[k]);
-        if (act != kNone) vload<T, VEC>(u + off, x[k]);
+        if (kAct) vload<T, VEC>(u + off, x[k]);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (yout) {
+        if (kAct && yout) {
           float a[VEC];
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) a[j] = act_f(act, x[k][j]);
+          for (int j = 0; j < VEC; ++j) {
+            float g;
+            act_fdf<ACT>(x[k][j], a[j], g);
+            d[k][j] *= g;
+          }
           vstore<T, VEC>(yout + (size_t)(r + k * stride) * cols + col, a);
-        }
-        if (act != kNone) {
+        } else if (kAct) {
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) d[k][j] *= act_df(act, x[k][j]);
+          for (int j = 0; j < VEC; ++j) d[k][j] *= act_df<ACT>(x[k][j]);
         }
         if (du) vstore<T, VEC>(du + (size_t)(r + k * stride) * cols + col, d[k]);
 #pragma unroll
@@ -108,17 +145,22 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, 
       const size_t off = (size_t)r * cols + col;
       float d[VEC];
       vload<T, VEC>(dy + off, d);
-      if (act != kNone) {
+      if (kAct) {
         float x[VEC];
         vload<T, VEC>(u + off, x);
         if (yout) {
           float a[VEC];
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) a[j] = act_f(act, x[j]);
+          for (int j = 0; j < VEC; ++j) {
+            float g;
+            act_fdf<ACT>(x[j], a[j], g);
+            d[j] *= g;
+          }
           vstore<T, VEC>(yout + off, a);
-        }
+        } else {
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) d[j] *= act_df(act, x[j]);
+          for (int j = 0; j < VEC; ++j) d[j] *= act_df<ACT>(x[j]);
+        }
       }
       if (du) vstore<T, VEC>(du + off, d);
 #pragma unroll
@@ -139,8 +181,16 @@ template <typename T, int VEC>
 void launch_act_bwd(const void* dy, const void* u, void* du, float* part, void* yout, int rows, int cols, int act,
                     int groups, hipStream_t s) {
   dim3 grid((cols / VEC + 63) / 64, groups);
-  hipLaunchKernelGGL((act_bwd_kernel<T, VEC>), grid, dim3(256), 0, s, (const T*)dy, (const T*)u, (T*)du, part,
-                     (T*)yout, rows, cols, act);
+#define DTD_ACT_BWD(A)                                                                                          \
+  hipLaunchKernelGGL((act_bwd_kernel<T, VEC, A>), grid, dim3(256), 0, s, (const T*)dy, (const T*)u, (T*)du, part, \
+                     (T*)yout, rows, cols)
+  switch (act) {
+    case kGeluErf: DTD_ACT_BWD(kGeluErf); break;
+    case kGeluTanh: DTD_ACT_BWD(kGeluTanh); break;
+    case kRelu: DTD_ACT_BWD(kRelu); break;
+    default: DTD_ACT_BWD(kNone); break;
+  }
+#undef DTD_ACT_BWD
 }
 
 template <typename T>
@@ -204,8 +254,17 @@ DTD_EXPORT int dtd_act_fwd(int dtype, const void* u, void* y, size_t n, int act,
   size_t blocks = (n / 8 + 255) / 256;
   if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;
-  if (dtype == kBF16) hipLaunchKernelGGL(act_fwd_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)u, (bf16*)y, n, act);
-  else hipLaunchKernelGGL(act_fwd_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)u, (float*)y, n, act);
+#define DTD_ACT_FWD(T, A) hipLaunchKernelGGL((act_fwd_kernel<T, A>), dim3(blocks), dim3(256), 0, s, (const T*)u, (T*)y, n)
+#define DTD_ACT_FWD_T(T)                                \
+  switch (act) {                                        \
+    case kGeluErf: DTD_ACT_FWD(T, kGeluErf); break;     \
+    case kGeluTanh: DTD_ACT_FWD(T, kGeluTanh); break;   \
+    case kRelu: DTD_ACT_FWD(T, kRelu); break;           \
+    default: DTD_ACT_FWD(T, kNone); break;              \
+  }
+  if (dtype == kBF16) { DTD_ACT_FWD_T(bf16) } else { DTD_ACT_FWD_T(float) }
+#undef DTD_ACT_FWD_T
+#undef DTD_ACT_FWD
   DTD_LAUNCH_CHECK();
 }
 

@@ -81,6 +81,25 @@ __device__ __forceinline__ float keep_bits(float v, uint32_t w, int b) {
   return __int_as_float(__float_as_int(v) & __builtin_amdgcn_sbfe((int)w, b, 1));
 }
 
+// Lane l <-> lane l^32 combine with v_permlane32_swap (a VALU op; __shfl_xor(x, 32) would be a
+// ds_bpermute round trip through the LDS pipe on the softmax critical path).
+__device__ __forceinline__ float xhalf_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// Keep word pre-shifted by 4*hh so the bit of accumulator register i is the compile-time
+// constant crow(i, 0): one v_bfe_i32 with inline offsets, no per-register bit-index VGPRs.
+__device__ __forceinline__ uint32_t half_word(uint32_t w, int hh) { return w >> (4 * hh); }
+// Defer-max threshold (log2 units, FwdArgs::thr): the running max is raised -- and O, l
+// rescaled -- only when some row's tile max exceeds it by more than this, so P = 2^(s - m)
+// stays <= 2^thr.  Default 8; DTD_ATTN_RESCALE_THR overrides it (0 = textbook online softmax,
+// used by the tests to check that deferral does not change the result beyond rounding).
+constexpr float kRescaleThr = 8.f;
+
 __device__ __forceinline__ float keep_of(const DropoutRng& g, uint64_t e, uint32_t thr) {
   const uint32_t b = g.bits(e >> 1);
   const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
@@ -91,7 +110,7 @@ struct FwdArgs {
   const bf16* q; const bf16* k; const bf16* v; bf16* o; float* lse; const float* slopes;
   const uint32_t* maskA;  // dropout keep bits [B*H][W][S]: bit j of word (w, q) = key 32w+j  (nullptr: no dropout)
   int B, S, H, ld, ldo, causal, W;
-  float scale, p;
+  float scale, p, thr;
 };
 
 // Dropout keep-masks for one attention call, generated once in a VALU-only pass at full
@@ -200,7 +219,11 @@ struct TileLoader {
 // double-buffered in LDS, fed by a 2-deep register ring of global loads: one barrier per tile.
 template <int D, int OCC, int BN>
 __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
-  constexpr int KP = D + 8, VP = D + 8, NC = D / 16, NDB = D / 32, NKB = BN / 32;
+  // K rows (ds_read_b128, 4x16-lane groups): pitch D+8 puts the 16 rows of a group on 16
+  // distinct 4-bank windows.  V (ds_read_b64_tr_b16, rows rr = 0..3 x column halves g = 0,1 per
+  // 32-lane group): pitch D+32 (48 / 80 dwords = 16 mod 64) places the eight 8-dword windows
+  // at distinct multiples of 8 mod 64 -- D+8 aliased rows 0/2 and 1/3 (2-way conflicts).
+  constexpr int KP = D + 8, VP = D + 32, NC = D / 16, NDB = D / 32, NKB = BN / 32;
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * VP];
 
@@ -302,33 +325,38 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
         for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, sacc[kb][i]);
       tmax *= sc2;
     }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(m, tmax);
-    const float alpha = fexp2(m - mnew);  // m = -inf on the first tile -> 0
-    m = mnew;
-    const float mexp = mnew == -INFINITY ? 0.f : mnew;
+    tmax = xhalf_max(tmax);
+    // defer-max (wave-uniform decision): keep the running max unless some row's tile max
+    // exceeds it by > kRescaleThr; the previous tile's P.V is complete, so O and l are the
+    // only terms at the old scale.  m = -inf (first tile / fully masked so far) -> alpha 0.
+    if (!__all(tmax - m <= a.thr)) {
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = m == -INFINITY ? 0.f : fexp2(m - mnew);
+      m = mnew;
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) oacc[d] *= alpha;
+    }
+    const float mexp = m == -INFINITY ? 0.f : m;
     const float msc = slow ? 1.f : sc2;
-    float psum = 0.f;
+    // l stays a per-half partial (both halves share m, hence every rescale); the two halves
+    // are combined once in the epilogue.  Four independent partial sums shorten the add chain.
+    float ps[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float pv = fexp2(fmaf(sacc[kb][i], msc, -mexp));
-        psum += pv;
+        ps[i & 3] += pv;
         sacc[kb][i] = pv;
       }
-    psum += __shfl_xor(psum, 32, 64);
-    l = l * alpha + psum;
-    if (alpha != 1.f) {
-#pragma unroll
-      for (int d = 0; d < NDB; ++d) oacc[d] *= alpha;
-    }
+    l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
     if (drop) {
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
-        const uint32_t mw = mwc[kb];
+        const uint32_t mw = half_word(mwc[kb], hh);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[kb][i] = keep_bits(sacc[kb][i], mw, crow(i, hh));
+        for (int i = 0; i < 16; ++i) sacc[kb][i] = keep_bits(sacc[kb][i], mw, crow(i, 0));
       }
     }
     // O^T += V^T . P^T: the score accumulator is the B operand; V^T comes from transposed reads
@@ -359,6 +387,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     tile(std::integral_constant<int, 1>{}, t);
     if (t + 1 < nt) tile(std::integral_constant<int, 0>{}, t + 1);
   }
+  l = xhalf_sum(l);
   if (!qvalid) return;
   const float inv_l = l > 0.f ? inv_keep / l : 0.f;   // dropout 1/(1-p) folded in here
   bf16* op = a.o + (size_t)(b * S + q) * a.ldo + h * D;
@@ -492,7 +521,11 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
     }
     const bf16* Q = Qs[buf];
     const bf16* O = Os[buf];
-#pragma unroll 1
+    // one wave per SIMD (OCC 1, 512 registers): unroll the query sub-blocks so the S/dP MFMAs
+    // of sub-block qb+1 can be scheduled under the softmax VALU of qb; at OCC 2 the register
+    // budget keeps the sub-blocks serial
+    constexpr int kQbUnroll = OCC == 1 ? BM / 32 : 1;
+#pragma unroll kQbUnroll
     for (int qb = 0; qb < BM / 32; ++qb) {
       f32x16 sacc = f32x16{}, pacc = f32x16{};
 #pragma unroll
@@ -506,6 +539,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       uint32_t mw = mwc[0];
 #pragma unroll
       for (int j = 1; j < NQW; ++j) mw = qb == j ? mwc[j] : mw;   // register select, no scratch
+      mw = half_word(mw, hh);
       // row statistics of this lane's 16 accumulator rows (rows 8g + 4hh + 0..3 are contiguous):
       // 8 ds_read_b128 issued together instead of 32 dependent scalar LDS reads
       f32x4 L4[4], D4[4];
@@ -527,8 +561,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       if (drop) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          pacc[i] = sacc[i] * fmaf(keep_bits(pacc[i], mw, crow(i, hh)), inv_keep, -D4[i >> 2][i & 3]);  // dS
-          sacc[i] = keep_bits(sacc[i], mw, crow(i, hh));                                          // P*mask (dV)
+          pacc[i] = sacc[i] * fmaf(keep_bits(pacc[i], mw, crow(i, 0)), inv_keep, -D4[i >> 2][i & 3]);  // dS
+          sacc[i] = keep_bits(sacc[i], mw, crow(i, 0));                                          // P*mask (dV)
         }
       } else {
 #pragma unroll
@@ -656,7 +690,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
         sacc = mfma32(*reinterpret_cast<const bf16x8*>(&K[(kb * 32 + r) * KP + 16 * c + 8 * hh]), qf[c], sacc);
         pacc = mfma32(*reinterpret_cast<const bf16x8*>(&V[(kb * 32 + r) * KP + 16 * c + 8 * hh]), of[c], pacc);
       }
-      const uint32_t mw = mwc[kb];
+      const uint32_t mw = half_word(mwc[kb], hh);
       // P = exp2(s*log2e - lse): 2 VALU on interior tiles without ALiBi
       if (needmask || sl2 != 0.f) {
 #pragma unroll
@@ -673,7 +707,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
       // dS^T = P * (dP - delta), dP = dropout(dP') (keep bit, 1/(1-p))
       if (drop) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[i] *= fmaf(keep_bits(pacc[i], mw, crow(i, hh)), inv_keep, -dl);
+        for (int i = 0; i < 16; ++i) sacc[i] *= fmaf(keep_bits(pacc[i], mw, crow(i, 0)), inv_keep, -dl);
       } else {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[i] *= pacc[i] - dl;
@@ -731,11 +765,12 @@ static int occupancy(int which) {
   return v[which];
 }
 
-// Keys per K/V tile of the head_dim-64 forward (which=0) and dQ (which=1) kernels: 64 (3 waves
-// per SIMD, 37 KB LDS) or 128 (2 waves per SIMD, 74 KB LDS; half the barriers per key).
+// Keys per K/V tile of the head_dim-64 forward (which=0) and dQ (which=1) kernels: 64 (37 KB
+// LDS) or 128 (74 KB LDS; half the barriers per key).  Measured on MI355X (scripts/bench_attn.py,
+// B=32): forward 64 (128 spills at 2 waves/SIMD), dQ 128 (-7 % backward time).
 // DTD_ATTN_TILE="f,q" overrides for tuning runs.
 static int tile_keys(int which) {
-  static const int defaults[2] = {64, 64};
+  static const int defaults[2] = {64, 128};
   const char* env = getenv("DTD_ATTN_TILE");
   if (!env) return defaults[which];
   int v[2] = {defaults[0], defaults[1]};
@@ -762,12 +797,15 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
                          keep_threshold(p));
     }
   }
+  const char* thr_env = getenv("DTD_ATTN_RESCALE_THR");
+  const float thr = thr_env ? (float)atof(thr_env) : kRescaleThr;
   FwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, slopes, mA, B, S, H, ld, ldo, causal, W,
-            scale, p};
+            scale, p, thr};
   dim3 grid((S + 127) / 128, B * H);
   if (D == 64) {
     const int o = occupancy(0);
-    if (tile_keys(0) == 128) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
+    if (tile_keys(0) == 128 && o == 1) hipLaunchKernelGGL((attn_fwd_kernel<64, 1, 128>), grid, dim3(256), 0, s, a);
+    else if (tile_keys(0) == 128) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
     else if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64>), grid, dim3(256), 0, s, a);
     else if (o == 2) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_fwd_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
@@ -810,11 +848,13 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
     // query tile of the dK/dV loop: 128 rows halves the barriers / exposed load latency per
     // query row at 2 blocks per CU (75 KB LDS each); DTD_ATTN_DKDV_BM=64 selects the old tile
     const int bm = getenv("DTD_ATTN_DKDV_BM") ? atoi(getenv("DTD_ATTN_DKDV_BM")) : 128;
-    if (bm == 128) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
+    if (bm == 128 && occupancy(1) == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 1, 128>), grid, dim3(256), 0, s, a);
+    else if (bm == 128) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
     else if (occupancy(1) >= 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
     const int o = occupancy(2);
-    if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
+    if (tile_keys(1) == 128 && o == 1) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 128>), grid, dim3(256), 0, s, a);
+    else if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
     else if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 64>), grid, dim3(256), 0, s, a);
     else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);

@@ -1,6 +1,10 @@
 #!/usr/bin/env python
 """Time the flash-attention kernels at the BERT-base training shape for several occupancy
-variants (DTD_ATTN_OCC="fwd,dkdv,dq" waves/SIMD).  Prints one JSON line per variant."""
+variants (DTD_ATTN_OCC="fwd,dkdv,dq" waves/SIMD).  Prints one JSON line per variant.
+
+fwd_us: forward kernel with the dropout keep bits generated ahead (as in the model, where the
+mask kernel runs on a side stream under the forward GEMMs); mask_us: the mask generator alone;
+bwd_us: delta + dK/dV + dQ."""
 import json
 import os
 import sys
@@ -34,12 +38,17 @@ def main():
     flops_f = 4 * B * H * S * S * D
     for occ in sys.argv[1:] or ["1,1,1", "2,2,2", "3,2,2", "3,2,3"]:
         os.environ["DTD_ATTN_OCC"] = occ
-        ctx, lse, mk = A.attn_fwd(qkv, B, S, H, D, False, None, p, rng, 3)
-        tf = timeit(lambda: A.attn_fwd(qkv, B, S, H, D, False, None, p, rng, 3))
+        pend = A.attn_masks_async(B, S, H, D, p, rng, 3, qkv.device) if p > 0 else None
+        torch.cuda.synchronize()
+        ctx, lse, mk = A.attn_fwd(qkv, B, S, H, D, False, None, p, rng, 3, masks=pend)
+        tf = timeit(lambda: A.attn_fwd(qkv, B, S, H, D, False, None, p, rng, 3, masks=pend))
+        cur = torch.cuda.current_stream()
+        tm = timeit(lambda: cur.wait_event(A.attn_masks_async(B, S, H, D, p, rng, 3, qkv.device).event)) \
+            if p > 0 else 0.0
         tb = timeit(lambda: A.attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, False, None, p, rng, 3, mk))
-        print(json.dumps({"occ": occ, "B": B, "p": p, "fwd_us": round(tf, 1), "bwd_us": round(tb, 1),
-                          "fwd_TFs": round(flops_f / tf / 1e6, 1), "bwd_TFs": round(2.5 * flops_f / tb / 1e6, 1)}),
-              flush=True)
+        print(json.dumps({"occ": occ, "B": B, "p": p, "fwd_us": round(tf, 1), "mask_us": round(tm, 1),
+                          "bwd_us": round(tb, 1), "fwd_TFs": round(flops_f / tf / 1e6, 1),
+                          "bwd_TFs": round(2.5 * flops_f / tb / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -62,3 +62,49 @@ def test_side_stream_masks_match_inline_generation():
     c2, l2, m2 = A.attn_fwd(qkv, B, S, H, D, False, None, p, rg, 4, masks=pend)
     torch.cuda.synchronize()
     assert torch.equal(m1, m2) and torch.equal(c1, c2) and torch.equal(l1, l2)
+
+
+def _spiked_qkv(B, S, H, D, spikes):
+    """Random q/k/v plus, in head 0, one query direction u shared by every query and keys
+    set to c*u at chosen positions: the running max of each query row jumps by ~11.5*c log2
+    units at those keys' tiles (c = 1 crosses the defer-max threshold, 0.5 stays under it)."""
+    torch.manual_seed(1)
+    x = (torch.randn(B, S, 3, H, D) * 0.5)
+    u = torch.ones(D)
+    x[:, :, 0, 0] = u
+    for key, c in spikes:
+        x[:, key, 1, 0] = c * u
+    return x.reshape(B * S, 3 * H * D).to(torch.bfloat16)
+
+
+def _fwd_fp64(qkv, B, S, H, D, causal):
+    x = qkv.double().view(B, S, 3, H, D)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    s = q @ k.transpose(-1, -2) / D ** 0.5
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool).triu(1), float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    ctx = torch.softmax(s, -1) @ v
+    return ctx.transpose(1, 2).reshape(B * S, H * D), lse
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_defer_max_rescale_branch_forced(monkeypatch, causal):
+    """SKILL rule 26: the defer-max rescale is data dependent.  Force it at chosen tiles (and a
+    sub-threshold growth in between), check the FULL output against an fp64 host reference,
+    and check that the shipped threshold and THR=0 (rescale on every growth) agree."""
+    B, S, H, D = 2, 512, 2, 64
+    qkv = _spiked_qkv(B, S, H, D, [(70, 1.0), (200, 1.5), (330, 2.5), (460, 2.6)])
+    ref_ctx, ref_lse = _fwd_fp64(qkv, B, S, H, D, causal)
+    outs = {}
+    for thr in ("0", "8", "1000"):
+        monkeypatch.setenv("DTD_ATTN_RESCALE_THR", thr)
+        ctx, lse, _ = A.attn_fwd(qkv.cuda(), B, S, H, D, causal, None, 0.0, None, 0)
+        torch.cuda.synchronize()
+        outs[thr] = (ctx.double().cpu(), lse.double().cpu())
+        assert torch.isfinite(outs[thr][0]).all()
+        err = (outs[thr][0] - ref_ctx).abs().max().item()
+        assert err < 3e-2, (thr, err)
+        assert (outs[thr][1] - ref_lse).abs().max().item() < 2e-2, thr
+    d = (outs["0"][0] - outs["8"][0]).abs().max().item()
+    assert d < 2e-2, d

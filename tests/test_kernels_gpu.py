@@ -92,6 +92,21 @@ def test_activation_fwd_bwd(act):
     assert torch.equal(res[DEV][0], res[DEV][3]) and torch.equal(res[DEV][1], res[DEV][4])
 
 
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh"])
+def test_activation_fast_math_accuracy_fp32(act):
+    """The kernels' one-exponential erf (A&S 7.1.26) and exp-based tanh vs float64 torch over
+    the range that matters (|x| <= 10, incl. the saturated tails)."""
+    x = torch.linspace(-10, 10, 200_003, dtype=torch.float64)
+    dy = torch.ones_like(x)
+    xr = x.clone().requires_grad_(True)
+    yr = torch.nn.functional.gelu(xr, approximate="none" if act == "gelu" else "tanh")
+    (gr,) = torch.autograd.grad(yr.sum(), xr)
+    y = Fx.act_fwd(x.float().to(DEV), act).double().cpu()
+    g = Fx.act_bwd(dy.float().to(DEV), x.float().to(DEV), act).double().cpu()
+    assert (y - yr.detach()).abs().max().item() < 2e-6
+    assert (g - gr).abs().max().item() < 2e-6
+
+
 @pytest.mark.parametrize("V", [28996, 50257, 1000, 250880])
 def test_softmax_xent(V):
     torch.manual_seed(2)
