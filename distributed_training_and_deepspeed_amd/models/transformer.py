@@ -26,7 +26,7 @@ from torch import nn
 from ..ops import attention as A
 from ..ops import functional as Fx
 from ..ops.grad import emit_wgrad, grad_done, grad_dst, note_use
-from ..ops.rng import RngState
+from ..ops.rng import RngState, attn_keep_mask
 from .config import TransformerConfig
 
 
@@ -85,6 +85,19 @@ def ref_dropout(x, p, training, rt: Runtime, sid):
     if rt.exact_dropout:
         return Fx._ref_dropout(x, p, rt.rng, sid)
     return F.dropout(x, p, True)
+
+
+def ref_attn_dropout(prob, p, training, rt: Runtime, sid):
+    """Attention-probability dropout [B, H, S, S] with the HIP mask generator's stream
+    (ops/rng.attn_keep_mask), so fused and reference models draw identical masks."""
+    if not training or p <= 0:
+        return prob
+    if rt.exact_dropout:
+        B, H, S, _ = prob.shape
+        seed, step = (int(v) for v in rt.rng.state.tolist())
+        keep = attn_keep_mask(B, H, S, p, seed, step, sid, device=prob.device)
+        return (prob.float() * keep / (1.0 - p)).to(prob.dtype)
+    return F.dropout(prob, p, True)
 
 
 class TransformerLayer(nn.Module):
@@ -165,7 +178,7 @@ class TransformerLayer(nn.Module):
             if c.causal:
                 s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
             prob = torch.softmax(s.float(), -1).to(s.dtype)
-            prob = ref_dropout(prob, p_a, tr, rt, rt.rng.sid(self.sid_attn))
+            prob = ref_attn_dropout(prob, p_a, tr, rt, rt.rng.sid(self.sid_attn))
             ctx = torch.matmul(prob, v).transpose(1, 2).reshape(B, S, h)
             return F.linear(ctx, self.o_w, self.o_b)
 

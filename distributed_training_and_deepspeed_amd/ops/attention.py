@@ -19,7 +19,7 @@ import math
 import torch
 
 from . import _lib
-from .rng import RngState, keep_mask
+from .rng import RngState, attn_keep_mask
 
 
 def alibi_slopes(num_heads: int) -> torch.Tensor:
@@ -54,7 +54,7 @@ def _scores(q, k, scale, causal, slopes):
 
 def _drop_mask(B, H, S, p, rng, sid, device):
     seed, step = (int(v) for v in rng.state.tolist())
-    return keep_mask(B * H * S * S, p, seed, step, sid, device=device).view(B, H, S, S)
+    return attn_keep_mask(B, H, S, p, seed, step, sid, device=device)
 
 
 def attn_fwd_ref(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | None = None, sid=0,

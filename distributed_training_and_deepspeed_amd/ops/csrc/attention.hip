@@ -113,63 +113,57 @@ struct FwdArgs {
   float scale, p, thr;
 };
 
+// v_writelane_b32 through the LLVM intrinsic (this clang has no __builtin for it; as a real
+// intrinsic the compiler still schedules it and pads its SGPR hazards, unlike inline asm).
+extern "C" __device__ uint32_t dtd_writelane(uint32_t val, uint32_t lane, uint32_t old) __asm("llvm.amdgcn.writelane.i32");
+
 // Dropout keep-masks for one attention call, generated once in a VALU-only pass at full
 // occupancy (instead of re-hashing inside the MFMA-bound forward, dK/dV and dQ kernels) and
 // stored as bits in two layouts so every consumer reads ONE 32-bit word per 32x32 tile:
 //   A [bh][w][q]  : bit j = key 32w+j   (forward / dQ: query on the lane)
-//   B [bh][w][key]: bit j = q   32w+j   (dK/dV: key on the lane) -- the transpose of A, formed
-//                   with wave ballots.
+//   B [bh][w][key]: bit j = q   32w+j   (dK/dV: key on the lane) -- the transpose of A.
 // Word-major ([w] outside the position) so that the 64 lanes of a consumer wave, which own 64
 // consecutive queries (keys), load one contiguous 256 B line per tile -- and the generator's
 // stores are contiguous too.
-// Keep(bh, q, key) = counter-RNG decision for flat element ((bh*S + q)*S + key), identical to
-// ops/rng.py keep_mask (so the math reference reproduces the masks bit for bit).
-// grid: (ceil(S/32), B*H); block: 256 = 4 waves; each wave covers 32 queries x 2 key-words per
-// iteration and strides over the key-word pairs (few, fat workgroups: the work per element is a
-// handful of VALU ops, so workgroup dispatch -- not math -- bounds a one-wave-per-tile grid).
+// Random stream (ops/rng.py attn_keep_mask, bit-identical): per (bh, q, 32-key word) one
+// counter hash seeds xorshift32; output n's low / high 16 bits decide keys 2n / 2n+1.
+// grid: (ceil(S/64), B*H); block 256 = 4 waves.  Lane = query (64 per wave); each wave walks
+// key words kw = wave, wave+4, ...  Per key the keep compare is ONE v_cmp whose lane mask is
+// both the A-bit (shifted into the lane's word) and, as a ballot, the B-words of 64 queries
+// (written into lane j / 32+j with v_writelane) -- no separate transpose pass.
 __global__ void __launch_bounds__(256) attn_mask_kernel(uint32_t* __restrict__ maskA, uint32_t* __restrict__ maskB,
                                                         int S, int W, const uint64_t* rng, uint32_t sid, uint32_t thr) {
   DropoutRng g(rng, sid);
   const int lane = threadIdx.x & 63, bh = blockIdx.y;
-  const int q = blockIdx.x * 32 + (lane & 31);
-  const uint64_t rowbase = ((uint64_t)bh * S + (uint64_t)(q < S ? q : 0)) * (uint64_t)S;
-  for (int kp = threadIdx.x >> 6; kp < (W + 1) / 2; kp += 4) {
-    const int kw = kp * 2 + (lane >> 5);
-    uint32_t word = 0;
-    if (q < S && kw < W) {
-      const uint64_t base = rowbase + (uint64_t)kw * 32;
-      const int nk = min(32, S - kw * 32);
-      const uint64_t i0 = base >> 1;
-      if ((base & 1) == 0 && (uint32_t)i0 <= 0xFFFFFFF0u) {   // 16 counters, one high word
-        const uint32_t ht = g.hi_term((uint32_t)(i0 >> 32)), lo0 = (uint32_t)i0;
-#pragma unroll 4
-        for (int j = 0; j < 32; j += 2) {
-          const uint32_t b = g.bits_lo(lo0 + (j >> 1), ht);
-          word |= (uint32_t)((b & 0xffffu) >= thr) << j;
-          word |= (uint32_t)((b >> 16) >= thr) << (j + 1);
-        }
-      } else {
-        for (int j = 0; j < 32; ++j) {
-          const uint64_t e = base + j;
-          const uint32_t b = g.bits(e >> 1);
-          const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
-          word |= (uint32_t)(h16 >= thr) << j;
-        }
-      }
-      if (nk < 32) word &= (nk > 0 ? (0xffffffffu >> (32 - nk)) : 0u);
-      maskA[((size_t)bh * W + kw) * S + q] = word;
-    }
-    // transpose through ballots: ballot j holds, for key-words kw0 (low half) and kw0+1 (high
-    // half), the q-bits of key 32*kw + j.  Lane j keeps the low word, lane 32+j the high word, so
-    // the 64 B-words leave in ONE store instruction.
-    uint32_t mine = 0;
+  const int q = blockIdx.x * 64 + lane;
+  const bool qv = q < S;
+  const uint64_t ctr0 = ((uint64_t)bh * S + (uint64_t)(qv ? q : 0)) * (uint64_t)W;
+  // keep(high half) <=> x >= thr << 16 <=> x > lim; keep(low half) <=> (x << 16) > lim.  Lanes
+  // past S (and p == 1) get lim = ~0: never kept, so their ballot bits are 0 with no extra op.
+  const uint32_t lim = (qv && thr <= 0xffffu) ? (thr << 16) - 1u : 0xffffffffu;
+  const int qw = blockIdx.x * 2 + (lane >> 5);   // query word of the B entry this lane stores
+  for (int kw = threadIdx.x >> 6; kw < W; kw += 4) {
+    uint32_t x = g.bits(ctr0 + kw);
+    x = x ? x : 0x6d2b79f5u;
+    uint32_t word = 0, bw = 0;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const unsigned long long bal = __ballot((word >> j) & 1u);
-      if ((lane & 31) == j) mine = (lane < 32) ? (uint32_t)bal : (uint32_t)(bal >> 32);
+    for (int n = 0; n < 16; ++n) {
+      if (n) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; }
+      const bool c0 = (x << 16) > lim;
+      const bool c1 = x > lim;
+      word |= (c0 ? 1u : 0u) << (2 * n);
+      word |= (c1 ? 1u : 0u) << (2 * n + 1);
+      const unsigned long long b0 = __ballot(c0), b1 = __ballot(c1);
+      bw = dtd_writelane((uint32_t)b0, 2 * n, bw);
+      bw = dtd_writelane((uint32_t)(b0 >> 32), 32 + 2 * n, bw);
+      bw = dtd_writelane((uint32_t)b1, 2 * n + 1, bw);
+      bw = dtd_writelane((uint32_t)(b1 >> 32), 32 + 2 * n + 1, bw);
     }
-    const int key = kp * 64 + lane;  // lane < 32: key-word kw0, lane >= 32: kw0 + 1
-    if (key < S) maskB[((size_t)bh * W + blockIdx.x) * S + key] = mine;
+    const int nk = S - kw * 32;                  // valid keys in this word
+    if (nk < 32) word &= (0xffffffffu >> (32 - nk));
+    if (qv) maskA[((size_t)bh * W + kw) * S + q] = word;
+    const int key = kw * 32 + (lane & 31);
+    if (key < S && qw < W) maskB[((size_t)bh * W + qw) * S + key] = bw;
   }
 }
 
@@ -793,7 +787,7 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
     // stream, overlapping the QKV GEMM)
     if (rng) {
       uint32_t* mB = masks + (size_t)B * H * S * W;
-      hipLaunchKernelGGL(attn_mask_kernel, dim3(W, B * H), dim3(256), 0, s, mA, mB, S, W, rng, sid,
+      hipLaunchKernelGGL(attn_mask_kernel, dim3((S + 63) / 64, B * H), dim3(256), 0, s, mA, mB, S, W, rng, sid,
                          keep_threshold(p));
     }
   }
@@ -824,8 +818,8 @@ DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, con
   if (B * S * H == 0 || p <= 0.f) return 0;
   if (!masks || !rng) return (int)hipErrorInvalidValue;
   const int W = (S + 31) / 32;
-  hipLaunchKernelGGL(attn_mask_kernel, dim3(W, B * H), dim3(256), 0, s, masks, masks + (size_t)B * H * S * W, S, W,
-                     rng, sid, keep_threshold(p));
+  hipLaunchKernelGGL(attn_mask_kernel, dim3((S + 63) / 64, B * H), dim3(256), 0, s, masks, masks + (size_t)B * H * S * W,
+                     S, W, rng, sid, keep_threshold(p));
   DTD_LAUNCH_CHECK();
 }
 

@@ -68,6 +68,39 @@ def keep_mask(numel: int, p: float, seed: int, step: int, sid: int, device="cpu"
     return h16 >= keep_threshold(p)
 
 
+def _xorshift32(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ ((x << 13) & M32)
+    x = x ^ (x >> 17)
+    x = x ^ ((x << 5) & M32)
+    return x
+
+
+def attn_keep_mask(B: int, H: int, S: int, p: float, seed: int, step: int, sid: int, device="cpu") -> torch.Tensor:
+    """Bool keep-mask [B, H, S, S] of attention-probability dropout (identical to the HIP mask
+    generator, ops/csrc/attention.hip ``attn_mask_kernel``).
+
+    Per (batch*head, query, 32-key word) one counter hash seeds an xorshift32 stream; its 16
+    outputs give the 32 keep decisions of the word (low / high 16 bits of output n -> keys
+    2n / 2n+1, keep iff >= the 16-bit threshold).  B*H*S*S decisions per layer make the
+    generator VALU-bound, so only one of every 16 32-bit draws pays for the full (two-multiply)
+    mix; the rest are three shift-xor pairs."""
+    k0, k1 = _keys(seed, step, sid)
+    W = (S + 31) // 32
+    ctr = torch.arange(B * H * S * W, dtype=torch.int64, device=device)
+    lo, hi = ctr & M32, ctr >> 32
+    x = _mix32(((lo ^ k0) + (((hi * 0xC2B2AE35) & M32) ^ k1)) & M32)
+    x = torch.where(x == 0, torch.full_like(x, 0x6D2B79F5), x)
+    thr = keep_threshold(p)
+    outs = []
+    for n in range(16):
+        if n:
+            x = _xorshift32(x)
+        outs.append((x & 0xFFFF) >= thr)
+        outs.append((x >> 16) >= thr)
+    keep = torch.stack(outs, -1).view(B, H, S, W * 32)
+    return keep[..., :S].contiguous()
+
+
 class RngState:
     """Device-resident {seed, step} for the dropout kernels plus the host-side micro-batch id."""
 
