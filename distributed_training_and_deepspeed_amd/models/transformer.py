@@ -314,7 +314,7 @@ class _FusedLayerFn(torch.autograd.Function):
                 grad_done(p)
         else:
             emit_wgrad(qkv_w, dqkv, x2d)
-            dx = torch.addmm(dz1, dqkv, qkv_w)
+            dx = dz1.addmm_(dqkv, qkv_w)   # in place: dz1 is this backward's own buffer (no C copy)
         return (dx.view(B, S, h), None) + (None,) * 12
 
 
