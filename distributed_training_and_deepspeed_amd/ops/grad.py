@@ -95,12 +95,17 @@ def wgrad_splits(tokens: int, out_f: int, in_f: int) -> int:
     768x3072 weight is 144 tiles of 128x128) while K = tokens is huge, so one GEMM leaves most
     of the 256 CUs idle.  Splitting K into s slices (one batched GEMM, then an fp32 sum) until
     there are >= 512 output tiles measured 1.6-2.6x faster on MI355X at 16k tokens
-    (scripts/bench_gemm.py); at <= 4k tokens a single GEMM is best."""
+    (scripts/bench_gemm.py); at <= 4k tokens a single GEMM is best.  At 64k tokens (b128) slices
+    of 4096 tokens (s = 16) beat the tile-count rule by 6-12 % per GEMM in isolation
+    (scripts/wgrad_sweep.py: QKV 270 -> 253 us, FC1/FC2 333 -> 317 us with fp32 partials,
+    235 / 294 us with bf16 partials)."""
     if tokens < 8192:
         return 1
     tiles = -(-out_f // 128) * -(-in_f // 128)
     s = 1
     while tiles * s < 512 and s < 16 and tokens % (2 * s) == 0 and tokens // (2 * s) >= 1024:
+        s *= 2
+    while s < 16 and tokens // (2 * s) >= 4096 and tokens % (2 * s) == 0:
         s *= 2
     return s
 
@@ -115,7 +120,7 @@ def emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         gemm_into(dst, dy.t(), x, acc)
     else:
         a, b = dy.view(s, T // s, o).transpose(1, 2), x.view(s, T // s, i)
-        part = _bmm_partials(a, b)
+        part = _bmm_partials(a, b, fp32=dst.dtype == torch.float32)
         splitk_reduce(part, dst, acc)
     grad_done(p)
 
@@ -123,10 +128,13 @@ def emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
 _F32_PARTIALS = [os.environ.get("DTD_WGRAD_F32_PARTIALS", "1") == "1"]
 
 
-def _bmm_partials(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """Batched K-slice products, in fp32 when hipBLASLt offers the bf16->fp32 batched GEMM
-    (no bf16 rounding of the partial sums), else in the input dtype."""
-    if _F32_PARTIALS[0] and a.dtype != torch.float32:
+def _bmm_partials(a: torch.Tensor, b: torch.Tensor, fp32: bool = True) -> torch.Tensor:
+    """Batched K-slice products.  The partials carry the destination's precision: fp32 (when
+    hipBLASLt offers the bf16->fp32 batched GEMM) for an fp32 gradient buffer, the input dtype
+    for a bf16 one -- there the final bf16 rounding dominates anyway (relative error 1.7e-3 with
+    fp32 partials vs 2.4e-3 with bf16 ones at 16 x 1024-token slices), and half the partial
+    traffic is +1.5 % BERT-base b128 throughput on MI355X (scripts/ab.py, same box)."""
+    if fp32 and _F32_PARTIALS[0] and a.dtype != torch.float32:
         try:
             return torch.bmm(a, b, out_dtype=torch.float32)
         except (RuntimeError, TypeError):

@@ -1,0 +1,91 @@
+#!/usr/bin/env python
+"""Same-box A/B of bench.py: MI355X boxes differ by a few % in absolute throughput, so a change
+is judged by alternating runs of the baseline variant and the candidate on one box.
+
+  python scripts/ab.py VARIANT [VARIANT ...] [--rounds N] [-- bench args]
+
+Variants are named patches applied in a fresh child process before bench.main() runs
+("base" = the tree as is).  Prints per-run values and the per-variant median."""
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _old_wgrad_split():
+    from distributed_training_and_deepspeed_amd.ops import grad as G
+
+    def old(tokens, out_f, in_f):
+        if tokens < 8192:
+            return 1
+        tiles = -(-out_f // 128) * -(-in_f // 128)
+        s = 1
+        while tiles * s < 512 and s < 16 and tokens % (2 * s) == 0 and tokens // (2 * s) >= 1024:
+            s *= 2
+        return s
+    G.wgrad_splits = old
+
+
+def _f32_wgrad_partials():
+    from distributed_training_and_deepspeed_amd.ops import grad as G
+    orig = G._bmm_partials
+    G._bmm_partials = lambda a, b, fp32=True: orig(a, b, True)
+
+
+def _no_keep_ffn_act():
+    from distributed_training_and_deepspeed_amd.models import transformer as T
+    orig = T.Runtime.__init__
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        self.keep_ffn_act = False
+    T.Runtime.__init__ = init
+
+
+PATCHES = {"base": lambda: None, "old_wgrad_split": _old_wgrad_split, "f32_wgrad_partials": _f32_wgrad_partials,
+           "no_keep_ffn_act": _no_keep_ffn_act}
+
+
+def child(variant, bench_args):
+    sys.path.insert(0, ROOT)
+    PATCHES[variant]()
+    sys.argv = ["bench.py"] + bench_args
+    import bench
+    bench.main()
+
+
+def main():
+    args = sys.argv[1:]
+    if args and args[0] == "--child":
+        child(args[1], args[2:])
+        return
+    bench_args = []
+    if "--" in args:
+        i = args.index("--")
+        args, bench_args = args[:i], args[i + 1:]
+    rounds = 2
+    if "--rounds" in args:
+        i = args.index("--rounds")
+        rounds = int(args[i + 1])
+        args = args[:i] + args[i + 2:]
+    variants = args or ["base"]
+    res = {v: [] for v in variants}
+    for _ in range(rounds):
+        for v in variants:
+            out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", v] + bench_args,
+                                 capture_output=True, text=True, timeout=600)
+            line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+            if out.returncode != 0 or not line:
+                print(json.dumps({"variant": v, "error": out.stderr[-500:]}), flush=True)
+                sys.exit(1)
+            val = json.loads(line[-1])["value"]
+            res[v].append(val)
+            print(json.dumps({"variant": v, "value": val}), flush=True)
+    print(json.dumps({"median": {v: statistics.median(x) for v, x in res.items()}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
