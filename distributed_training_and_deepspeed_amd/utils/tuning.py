@@ -25,7 +25,7 @@ DEFAULT_TABLE = Path(__file__).resolve().parent.parent / "tuning" / "tunableop_m
 def use_tuned_gemms(path: str | os.PathLike | None = None) -> bool:
     if not torch.cuda.is_available() or torch.version.hip is None:
         return False
-    path = Path(path) if path else DEFAULT_TABLE
+    path = Path(path or os.environ.get("DTD_TUNED_TABLE") or DEFAULT_TABLE)
     if not path.exists():
         return False
     try:

@@ -45,7 +45,11 @@ def _no_keep_ffn_act():
     T.Runtime.__init__ = init
 
 
-PATCHES = {"base": lambda: None, "old_wgrad_split": _old_wgrad_split, "f32_wgrad_partials": _f32_wgrad_partials,
+def _no_tuned():
+    os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "0"
+
+
+PATCHES = {"no_tuned": _no_tuned, "base": lambda: None, "old_wgrad_split": _old_wgrad_split, "f32_wgrad_partials": _f32_wgrad_partials,
            "no_keep_ffn_act": _no_keep_ffn_act}
 
 
