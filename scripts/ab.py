@@ -49,14 +49,22 @@ def _no_tuned():
     os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "0"
 
 
-PATCHES = {"no_tuned": _no_tuned, "base": lambda: None, "old_wgrad_split": _old_wgrad_split, "f32_wgrad_partials": _f32_wgrad_partials,
+def _env(**kv):
+    def f():
+        os.environ.update(kv)
+    return f
+
+
+PATCHES = {"no_tuned": _no_tuned, "graph": lambda: ["--graph", "on"],
+           "attn_occ_323": _env(DTD_ATTN_OCC="3,2,3"), "attn_occ_222_dq64": _env(DTD_ATTN_TILE="64,64"),
+           "base": lambda: None, "old_wgrad_split": _old_wgrad_split, "f32_wgrad_partials": _f32_wgrad_partials,
            "no_keep_ffn_act": _no_keep_ffn_act}
 
 
 def child(variant, bench_args):
     sys.path.insert(0, ROOT)
-    PATCHES[variant]()
-    sys.argv = ["bench.py"] + bench_args
+    extra = PATCHES[variant]() or []
+    sys.argv = ["bench.py"] + bench_args + list(extra)
     import bench
     bench.main()
 
