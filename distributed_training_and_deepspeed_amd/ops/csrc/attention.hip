@@ -211,7 +211,7 @@ struct TileLoader {
 
 // grid: (ceil(S/128), B*H); block 256 = 4 waves x 32 queries.  KV tiles of BN keys,
 // double-buffered in LDS, fed by a 2-deep register ring of global loads: one barrier per tile.
-template <int D, int OCC, int BN>
+template <int D, int OCC, int BN, int RING>
 __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   // K rows (ds_read_b128, 4x16-lane groups): pitch D+8 puts the 16 rows of a group on 16
   // distinct 4-bank windows.  V (ds_read_b64_tr_b16, rows rr = 0..3 x column halves g = 0,1 per
@@ -254,8 +254,13 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   // tile t is computed and written to LDS only at the end of tile t+1, so each load has two
   // tiles of compute to arrive (one tile of MFMA/softmax work is shorter than an HBM round trip).
   // The dropout keep words (one per 32 keys) ride along in the same ring.
-  TileLoader<D, BN> kl0, vl0, kl1, vl1;
-  uint32_t mwc[NKB], mw0[NKB], mw1[NKB];
+  // RING = 1: one register set (tile t+1 in flight during tile t) -- 16 fewer VGPRs at BN = 64,
+  // which is what 3 waves per SIMD needs.
+  TileLoader<D, BN> kl0, vl0, kl1r, vl1r;
+  TileLoader<D, BN>& kl1 = RING == 2 ? kl1r : kl0;
+  TileLoader<D, BN>& vl1 = RING == 2 ? vl1r : vl0;
+  uint32_t mwc[NKB], mw0[NKB], mw1r[NKB];
+  uint32_t* mw1 = RING == 2 ? mw1r : mw0;
   // unconditional word loads (a valid dummy address without dropout) keep the ring branch-free
   const uint32_t* wbase = drop ? mcol : reinterpret_cast<const uint32_t*>(a.lse);
   const size_t wstride = drop ? (size_t)S : 0;
@@ -274,7 +279,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   {
     const int k1 = min(1, nt - 1) * BN, k2 = min(2, nt - 1) * BN;
     kl1.load(kbase, a.ld, k1, S); vl1.load(vbase, a.ld, k1, S); load_words(k1, mw1);
-    kl0.load(kbase, a.ld, k2, S); vl0.load(vbase, a.ld, k2, S); load_words(k2, mw0);
+    if constexpr (RING == 2) { kl0.load(kbase, a.ld, k2, S); vl0.load(vbase, a.ld, k2, S); load_words(k2, mw0); }
   }
   __syncthreads();
   // SET = register set holding tile t+1 (t even -> 1, t odd -> 0)
@@ -369,8 +374,8 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
       vn.store(Vs[buf ^ 1], VP);
 #pragma unroll
       for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
-      // tile t+3 (clamped to the last tile: a harmless reload keeps the issue unconditional)
-      const int kf = min(t + 3, nt - 1) * BN;
+      // tile t+1+RING (clamped to the last tile: a harmless reload keeps the issue unconditional)
+      const int kf = min(t + 1 + RING, nt - 1) * BN;
       kn.load(kbase, a.ld, kf, S);
       vn.load(vbase, a.ld, kf, S);
       load_words(kf, mwn);
@@ -602,7 +607,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
 // dQ: grid (ceil(S/128), B*H); block 256 = 4 waves x 32 queries (query on the lane, as in the
 // forward); recomputes S^T and dP^T per 64-key tile and accumulates dQ^T = K^T.dS^T in
 // registers -- no atomics, no cross-workgroup reduction.
-template <int D, int OCC, int BN>
+template <int D, int OCC, int BN, int RING>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   constexpr int KP = D + 8, NC = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
@@ -644,8 +649,12 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   const int nt = (kend + BN - 1) / BN;
   // K/V tiles + dropout keep words through a 2-deep register ring (see attn_fwd_kernel)
   constexpr int NKB = BN / 32;
-  TileLoader<D, BN> kl0, vl0, kl1, vl1;
-  uint32_t mwc[NKB], mw0[NKB], mw1[NKB];
+  // RING = 1: one register set in flight (fewer VGPRs -> 3 waves per SIMD), see attn_fwd_kernel
+  TileLoader<D, BN> kl0, vl0, kl1r, vl1r;
+  TileLoader<D, BN>& kl1 = RING == 2 ? kl1r : kl0;
+  TileLoader<D, BN>& vl1 = RING == 2 ? vl1r : vl0;
+  uint32_t mwc[NKB], mw0[NKB], mw1r[NKB];
+  uint32_t* mw1 = RING == 2 ? mw1r : mw0;
   // unconditional word loads (a valid dummy address without dropout) keep the ring branch-free
   const uint32_t* wbase = drop ? mcol : reinterpret_cast<const uint32_t*>(a.lse);
   const size_t wstride = drop ? (size_t)S : 0;
@@ -664,7 +673,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   {
     const int k1 = min(1, nt - 1) * BN, k2 = min(2, nt - 1) * BN;
     kl1.load(kbase, a.ld, k1, S); vl1.load(vbase, a.ld, k1, S); load_words(k1, mw1);
-    kl0.load(kbase, a.ld, k2, S); vl0.load(vbase, a.ld, k2, S); load_words(k2, mw0);
+    if constexpr (RING == 2) { kl0.load(kbase, a.ld, k2, S); vl0.load(vbase, a.ld, k2, S); load_words(k2, mw0); }
   }
   __syncthreads();
   auto tile = [&](auto set_c, int t) {
@@ -720,8 +729,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
       vn.store(Vs[buf ^ 1], KP);
 #pragma unroll
       for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
-      // tile t+3 (clamped to the last tile: a harmless reload keeps the issue unconditional)
-      const int kf = min(t + 3, nt - 1) * BN;
+      // tile t+1+RING (clamped to the last tile: a harmless reload keeps the issue unconditional)
+      const int kf = min(t + 1 + RING, nt - 1) * BN;
       kn.load(kbase, a.ld, kf, S);
       vn.load(vbase, a.ld, kf, S);
       load_words(kf, mwn);
@@ -748,10 +757,14 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
 }  // namespace
 
 // Waves per SIMD the head_dim-64 kernels are compiled for (register budget 512/OCC per lane):
-// fwd, dK/dV, dQ.  Defaults are the measured best on MI355X (scripts/bench_attn.py); override
-// with DTD_ATTN_OCC="f,kv,q" for tuning runs.
+// fwd, dK/dV, dQ.  The kernels are latency-bound (dependent MFMA -> softmax -> MFMA chains per
+// wave), so waves per SIMD matter more than in-flight tile loads: at 3 waves the forward and dQ
+// keep ONE register set of the next K/V tile in flight (RING = 1, 166-168 VGPRs, no spills)
+// instead of two -- forward 233 -> 188 us at B=128 (scripts/bench_attn.py), +1.4 % whole-step
+// throughput same-box (profiles/r1_ab_attn_occ.jsonl).  dK/dV stays at 2 (255 VGPRs).
+// Override with DTD_ATTN_OCC="f,kv,q" for tuning runs.
 static int occupancy(int which) {
-  static const int defaults[3] = {2, 2, 2};
+  static const int defaults[3] = {3, 2, 3};
   const char* env = getenv("DTD_ATTN_OCC");
   if (!env) return defaults[which];
   int v[3] = {defaults[0], defaults[1], defaults[2]};
@@ -760,11 +773,11 @@ static int occupancy(int which) {
 }
 
 // Keys per K/V tile of the head_dim-64 forward (which=0) and dQ (which=1) kernels: 64 (37 KB
-// LDS) or 128 (74 KB LDS; half the barriers per key).  Measured on MI355X (scripts/bench_attn.py,
-// B=32): forward 64 (128 spills at 2 waves/SIMD), dQ 128 (-7 % backward time).
+// LDS) or 128 (74 KB LDS; half the barriers per key, but 2 waves/SIMD at most).  64 for both
+// with the 3-wave kernels (128-key dQ at 2 waves: 3 % slower backward).
 // DTD_ATTN_TILE="f,q" overrides for tuning runs.
 static int tile_keys(int which) {
-  static const int defaults[2] = {64, 128};
+  static const int defaults[2] = {64, 64};
   const char* env = getenv("DTD_ATTN_TILE");
   if (!env) return defaults[which];
   int v[2] = {defaults[0], defaults[1]};
@@ -798,13 +811,12 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
   dim3 grid((S + 127) / 128, B * H);
   if (D == 64) {
     const int o = occupancy(0);
-    if (tile_keys(0) == 128 && o == 1) hipLaunchKernelGGL((attn_fwd_kernel<64, 1, 128>), grid, dim3(256), 0, s, a);
-    else if (tile_keys(0) == 128) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
-    else if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64>), grid, dim3(256), 0, s, a);
-    else if (o == 2) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
+    if (tile_keys(0) == 128) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 128, 2>), grid, dim3(256), 0, s, a);
+    else if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
+    else if (o == 2) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 64, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<64, 1, 64, 2>), grid, dim3(256), 0, s, a);
   } else if (D == 128) {
-    hipLaunchKernelGGL((attn_fwd_kernel<128, 1, 64>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<128, 1, 64, 2>), grid, dim3(256), 0, s, a);
   } else {
     return (int)hipErrorInvalidValue;
   }
@@ -847,15 +859,15 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
     else if (occupancy(1) >= 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
     const int o = occupancy(2);
-    if (tile_keys(1) == 128 && o == 1) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 128>), grid, dim3(256), 0, s, a);
-    else if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
-    else if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 64>), grid, dim3(256), 0, s, a);
-    else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
+    if (tile_keys(1) == 128 && o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 128, 1>), grid, dim3(256), 0, s, a);
+    else if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128, 2>), grid, dim3(256), 0, s, a);
+    else if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
+    else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 64, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 64, 2>), grid, dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL(attn_bwd_delta_kernel<128>, dim3((unsigned)(((long long)B * S * H * 16 + 255) / 256)), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<128, 1, 64>), grid, dim3(256), 0, s, a);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<128, 1, 64>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<128, 1, 64, 2>), grid, dim3(256), 0, s, a);
   }
   DTD_LAUNCH_CHECK();
 }
