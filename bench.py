@@ -7,8 +7,9 @@ timed here is the full training step of the reference's ``data_parallel_training
 bert-base-cased geometry (108.3 M parameters, random init), seq 512, synthetic MLM batches
 with the reference masking law, bf16 compute with fp32 master weights.  Per-GPU batch is
 fixed as N grows (weak scaling); the default 128 x 512 tokens per GPU (the reference ran 4 on a
-16 GB T4) uses ~30 GB of the 288 GB HBM, runs the GEMMs at their large-M efficiency
-(1.3-1.5 PF/s) and amortises the per-step gradient all-reduce over a 60 ms step.
+16 GB T4) uses ~35 GB of the 288 GB HBM, runs the GEMMs at their large-M efficiency
+(1.0-1.4 PF/s) and amortises the per-step gradient all-reduce over a ~55 ms step.  Each rank
+draws its own dropout masks (seed offset by rank).
 
   python bench.py --gpus N --steps K --warmup W
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -82,6 +83,7 @@ def main():
     if args.impl == "reference":
         model.rt.exact_dropout = False  # torch-eager baseline: ATen dropout, HF-style eager ops
     model.train()
+    model.rt.rng.reseed(1234 + rank)   # independent dropout masks per data-parallel replica
     gdt = {"bf16": torch.bfloat16, "fp32": torch.float32}.get(args.grad_dtype, dtype)
     ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt,
                                   small_bucket_allreduce=args.small_bucket_allreduce)

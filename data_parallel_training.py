@@ -44,6 +44,7 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
     cfg = get_config(name)
     model = build_model(name, dtype=dtype, device=device, seed=0, impl=opts.impl)
     model.train()
+    model.rt.rng.reseed(rank)   # independent dropout masks per replica (parameters are broadcast)
     ddp = DistributedDataParallel(model, bucket_cap_mb=bucket_size,
                                   grad_dtype={"bf16": torch.bfloat16, "fp32": torch.float32}.get(opts.grad_dtype, dtype))
     optimizer = hf_adamw(ddp.parameters(), lr=5e-5)
@@ -65,21 +66,37 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
             pass
     if opts.markers:
         enable_markers()
+    def step(input_ids, labels):
+        with marker("forward"):
+            out = ddp(input_ids, labels=labels)
+        with marker("backward+allreduce"):
+            out.loss.backward()
+        with marker("optimizer"):
+            optimizer.step()
+            optimizer.zero_grad()
+            model.rt.rng.advance()
+        return out.loss.detach()
+
+    graphed = None
+    if opts.graph and cuda:
+        # whole step (forward, backward + bucket all-reduces, optimizer, RNG advance) replayed as
+        # one hipGraph: the reference's 4 x 512-token batches are host-launch bound otherwise
+        from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep, mlm_capacity
+        model.rt.mlm_capacity = mlm_capacity(batch_size * opts.seq_len)
+        ex = dataset[0:batch_size]
+        graphed = CapturedStep(step, {"input_ids": ex["input_ids"].to(device), "labels": ex["labels"].to(device)},
+                               runtime=model.rt)
+
     timer = StepTimer(batch_size * opts.seq_len, world_size)
     start = time.time()
     n = 0
     loss = None
     for batch in loader:
         timer.start()
-        with marker("forward"):
-            out = ddp(batch["input_ids"], labels=batch["labels"])
-            loss = out.loss
-        with marker("backward+allreduce"):
-            loss.backward()
-        with marker("optimizer"):
-            optimizer.step()
-            optimizer.zero_grad()
-            model.rt.rng.advance()
+        if graphed is not None and batch["input_ids"].shape == graphed.static["input_ids"].shape:
+            loss = graphed(input_ids=batch["input_ids"], labels=batch["labels"])
+        else:
+            loss = step(batch["input_ids"], batch["labels"])
         timer.stop()
         n += 1
         if progress is not None:
@@ -87,6 +104,8 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
     if cuda:
         torch.cuda.synchronize()
     elapsed = time.time() - start
+    if graphed is not None:
+        graphed.check()
     if opts.save_dir:
         save_checkpoint(os.path.join(opts.save_dir, "ddp_checkpoint.pt"), model, optimizer, step=n)
     print(f"\nTotal Training Time: {elapsed:.2f} seconds")
@@ -117,6 +136,8 @@ if __name__ == "__main__":
     parser.add_argument("--markers", action="store_true", help="roctx ranges per phase (rocprofv3 --marker-trace)")
     parser.add_argument("--save-dir", default="", help="write <dir>/ddp_checkpoint.pt at the end")
     parser.add_argument("--resume", default="", help="checkpoint file to resume from")
+    parser.add_argument("--graph", action="store_true",
+                        help="capture the whole training step in a hipGraph and replay it (small batches)")
     args = parser.parse_args()
 
     device_count = args.device_count or get_device_count()

@@ -115,6 +115,14 @@ class RngState:
         self.state = self.state.to(self.device)
         return self
 
+    def reseed(self, seed: int) -> "RngState":
+        """New dropout seed, in place (keeps the device tensor, so captured graphs stay valid).
+        Data-parallel trainers offset it by rank: replicas then draw independent masks, as
+        unseeded per-process RNGs do in the reference's torch DDP runs."""
+        self.seed = int(seed) & 0x7FFFFFFFFFFFFFFF
+        self.state.copy_(torch.tensor([self.seed, 0], dtype=torch.int64))
+        return self
+
     def advance(self) -> None:
         """Next training step (device op: graph-capturable)."""
         self.state[1:2].add_(1)
