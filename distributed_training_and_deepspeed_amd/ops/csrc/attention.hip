@@ -402,37 +402,9 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   if (hh == 0) a.lse[(size_t)bh * S + q] = (m + log2f(l)) * kLn2;
 }
 
-// delta[b,h,q] = sum_d dO[q,d] * O[q,d]  (one wave per (row, head))
-template <int D>
-__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout,
-                                                             float* __restrict__ delta, int B, int S, int H, int ldo) {
-  // one thread = 8 contiguous elements (16-byte loads); D/8 threads per (row, head) reduce with
-  // xor shuffles.  256 threads cover 256*8/D (row, head) pairs.
-  constexpr int TPH = D / 8;
-  const long long pair = ((long long)blockIdx.x * 256 + threadIdx.x) / TPH;  // (row, head) index
-  const int sub = threadIdx.x % TPH;
-  const long long npairs = (long long)B * S * H;
-  float acc = 0.f;
-  if (pair < npairs) {
-    const int row = (int)(pair / H), h = (int)(pair % H);
-    const size_t off = (size_t)row * ldo + h * D + sub * 8;
-    float x[8], y[8];
-    vload<bf16, 8>(o + off, x);
-    vload<bf16, 8>(dout + off, y);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
-  }
-#pragma unroll
-  for (int m = TPH / 2; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
-  if (pair < npairs && sub == 0) {
-    const int row = (int)(pair / H), h = (int)(pair % H);
-    const int b = row / S, sq = row % S;
-    delta[((size_t)b * H + h) * S + sq] = acc;
-  }
-}
-
 struct BwdArgs {
-  const bf16* q; const bf16* k; const bf16* v; const bf16* dout; const float* lse; const float* delta;
+  const bf16* q; const bf16* k; const bf16* v; const bf16* dout; const float* lse; float* delta;
+  const bf16* o;   // forward output: the dQ kernel forms delta = rowsum(dO * O) from it
   bf16* dq; bf16* dk; bf16* dv; const float* slopes;
   const uint32_t* maskA; const uint32_t* maskB;  // dropout keep bits (see attn_mask_kernel)
   int B, S, H, ld, ldo, causal, W;
@@ -640,7 +612,22 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
     }
   }
   const float lse2 = qvalid ? a.lse[(size_t)bh * S + q] * kLog2e : 0.f;
-  const float dl = qvalid ? a.delta[(size_t)bh * S + q] : 0.f;
+  // delta = rowsum(dO * O) of this lane's query, from the dO fragments already in registers and
+  // one O row read (no separate delta pass re-reading dO); stored for the dK/dV kernel, which
+  // runs after this one
+  float dl;
+  {
+    const bf16* orow = a.o + ((size_t)(b * S + (qvalid ? q : 0)) * a.ldo + h * D);
+    float part = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const bf16x8 ov = qvalid ? *reinterpret_cast<const bf16x8*>(orow + 16 * c + 8 * hh) : bf16x8{};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part = fmaf((float)ov[j], (float)of[c][j], part);
+    }
+    dl = xhalf_sum(part);
+    if (qvalid && hh == 0) a.delta[(size_t)bh * S + q] = dl;
+  }
   f32x16 dq[NDB];
 #pragma unroll
   for (int d = 0; d < NDB; ++d) dq[d] = f32x16{};
@@ -847,10 +834,16 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   const uint32_t* mB = (p > 0.f) ? masks + (size_t)B * H * S * W : nullptr;
   if (p > 0.f && !masks) return (int)hipErrorInvalidValue;
   dim3 grid((S + 127) / 128, B * H);
-  BwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, (bf16*)dk,
-            (bf16*)dv, slopes, mA, mB, B, S, H, ld, ldo, causal, W, scale, p};
+  BwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (const bf16*)o,
+            (bf16*)dq, (bf16*)dk, (bf16*)dv, slopes, mA, mB, B, S, H, ld, ldo, causal, W, scale, p};
+  // dQ first: it also produces delta = rowsum(dO * O), which the dK/dV kernel then reads
   if (D == 64) {
-    hipLaunchKernelGGL(attn_bwd_delta_kernel<64>, dim3((unsigned)(((long long)B * S * H * 8 + 255) / 256)), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
+    const int o = occupancy(2);
+    if (tile_keys(1) == 128 && o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 128, 1>), grid, dim3(256), 0, s, a);
+    else if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128, 2>), grid, dim3(256), 0, s, a);
+    else if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
+    else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 64, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 64, 2>), grid, dim3(256), 0, s, a);
     // query tile of the dK/dV loop: 128 rows halves the barriers / exposed load latency per
     // query row at 2 blocks per CU (75 KB LDS each); DTD_ATTN_DKDV_BM=64 selects the old tile
     const int bm = getenv("DTD_ATTN_DKDV_BM") ? atoi(getenv("DTD_ATTN_DKDV_BM")) : 128;
@@ -858,16 +851,9 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
     else if (bm == 128) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
     else if (occupancy(1) >= 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
-    const int o = occupancy(2);
-    if (tile_keys(1) == 128 && o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 128, 1>), grid, dim3(256), 0, s, a);
-    else if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128, 2>), grid, dim3(256), 0, s, a);
-    else if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
-    else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 64, 2>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 64, 2>), grid, dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL(attn_bwd_delta_kernel<128>, dim3((unsigned)(((long long)B * S * H * 16 + 255) / 256)), dim3(256), 0, s, (const bf16*)o, (const bf16*)dout, delta, B, S, H, ldo);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<128, 1, 64>), grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<128, 1, 64, 2>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<128, 1, 64>), grid, dim3(256), 0, s, a);
   }
   DTD_LAUNCH_CHECK();
 }
