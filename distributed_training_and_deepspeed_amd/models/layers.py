@@ -314,26 +314,6 @@ class LMHead(nn.Module):
     def logits(self, x):
         return F.linear(x, self.weight)
 
-    def _gather_labelled(self, x2: torch.Tensor, lab: torch.Tensor):
-        """Rows with a label (~15% under MLM): the head GEMMs, CE and their backward run on
-        these only.  With ``rt.mlm_capacity`` the gather has a static size (HIP-graph
-        capturable): padding rows point at row 0 with label -100 (zero loss / gradient), and
-        ``rt.mlm_overflow`` records on the device whether a batch had more labelled rows than
-        the capacity (the caller checks it; identical loss and gradients otherwise)."""
-        valid = lab != Fx.IGNORE_INDEX
-        cap = self.rt.mlm_capacity
-        if cap is None:
-            idx = valid.nonzero().squeeze(1)
-            return x2.index_select(0, idx), lab.index_select(0, idx)
-        cap = min(cap, lab.numel())
-        idx = torch.nonzero_static(valid, size=cap, fill_value=0).squeeze(1)
-        count = valid.sum()
-        keep = torch.arange(cap, device=lab.device) < count
-        lab_sel = torch.where(keep, lab.index_select(0, idx), torch.full_like(idx, Fx.IGNORE_INDEX))
-        if self.rt.mlm_overflow is not None:
-            self.rt.mlm_overflow.logical_or_(count > cap)
-        return x2.index_select(0, idx), lab_sel
-
     def loss(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         """HF causal-LM loss: logits[:, :-1] vs labels[:, 1:], ignore_index -100."""
         B, S, h = x.shape

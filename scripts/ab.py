@@ -49,13 +49,25 @@ def _no_tuned():
     os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "0"
 
 
+def _mlm_static():
+    # static-capacity sparse MLM head in eager mode (no nonzero() host sync per step)
+    from distributed_training_and_deepspeed_amd.models import transformer as T
+    from distributed_training_and_deepspeed_amd.utils.graphs import mlm_capacity
+    orig = T.Runtime.__init__
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        self.mlm_capacity = mlm_capacity(128 * 512)
+    T.Runtime.__init__ = init
+
+
 def _env(**kv):
     def f():
         os.environ.update(kv)
     return f
 
 
-PATCHES = {"no_tuned": _no_tuned, "graph": lambda: ["--graph", "on"],
+PATCHES = {"no_tuned": _no_tuned, "mlm_static": _mlm_static, "graph": lambda: ["--graph", "on"],
            "attn_occ_323": _env(DTD_ATTN_OCC="3,2,3"), "attn_occ_222_dq64": _env(DTD_ATTN_TILE="64,64"),
            "attn_occ_322": _env(DTD_ATTN_OCC="3,2,2"), "attn_occ_323_dq64": _env(DTD_ATTN_OCC="3,2,3", DTD_ATTN_TILE="64,64"),
            "base": lambda: None, "old_wgrad_split": _old_wgrad_split, "f32_wgrad_partials": _f32_wgrad_partials,
