@@ -759,9 +759,10 @@ static int occupancy(int which) {
   return v[which];
 }
 
-// Keys per K/V tile of the head_dim-64 forward (which=0) and dQ (which=1) kernels: 64 (37 KB
-// LDS) or 128 (74 KB LDS; half the barriers per key, but 2 waves/SIMD at most).  64 for both
-// with the 3-wave kernels (128-key dQ at 2 waves: 3 % slower backward).
+// Keys per K/V tile of the dQ kernel (which=1; the forward uses 64): 64 (37 KB LDS) or 128
+// (74 KB LDS; half the barriers per key, but 2 waves/SIMD at most).  64 with the 3-wave kernel
+// (128-key dQ at 2 waves: 3 % slower backward).  Measured and dropped: 128-key forward tiles
+// (spill at 2 waves), 32-key forward tiles at 4 waves/SIMD (120 VGPRs; 7 % slower than 64 at 3).
 // DTD_ATTN_TILE="f,q" overrides for tuning runs.
 static int tile_keys(int which) {
   static const int defaults[2] = {64, 64};
@@ -798,8 +799,7 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
   dim3 grid((S + 127) / 128, B * H);
   if (D == 64) {
     const int o = occupancy(0);
-    if (tile_keys(0) == 128) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 128, 2>), grid, dim3(256), 0, s, a);
-    else if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
+    if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
     else if (o == 2) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 64, 2>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_fwd_kernel<64, 1, 64, 2>), grid, dim3(256), 0, s, a);
   } else if (D == 128) {
@@ -839,8 +839,7 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   // dQ first: it also produces delta = rowsum(dO * O), which the dK/dV kernel then reads
   if (D == 64) {
     const int o = occupancy(2);
-    if (tile_keys(1) == 128 && o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 128, 1>), grid, dim3(256), 0, s, a);
-    else if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128, 2>), grid, dim3(256), 0, s, a);
+    if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128, 2>), grid, dim3(256), 0, s, a);
     else if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
     else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 64, 2>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 64, 2>), grid, dim3(256), 0, s, a);
