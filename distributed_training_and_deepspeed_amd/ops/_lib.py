@@ -59,6 +59,10 @@ _SIGS = {
     # softmax.hip
     "dtd_softmax_fwd": (I, [I, P, P, I, I, P]),
     "dtd_softmax_bwd": (I, [I, P, P, P, I, I, P]),
+    # gemm.hip
+    "dtd_gemm_bt_supported": (I, [I, I, I]),
+    "dtd_gemm_bt_part_rows": (I, [I]),
+    "dtd_gemm_bt": (I, [I, P, I, P, I, P, I, P, P, I, P, P, I, I, I, P]),
     # reduce.hip
     "dtd_splitk_reduce": (I, [P, I, I, ctypes.c_longlong, P, I, I, P]),
 }
