@@ -74,53 +74,73 @@ __global__ void __launch_bounds__(256) embed_word_bwd_kernel(const int64_t* __re
 // per chunk), pass 2 adds a segment's chunk sums in order into the table row.  seg_lo/seg_hi
 // are the [first, last+1) sorted positions of each position's id (searchsorted left/right).
 constexpr int kChunk = 16;
+// Chunk length of a segment: at least kChunk, and ~sqrt(len) for long ones, so neither pass
+// sums more than ~sqrt(len) rows serially in one wave (synthetic MLM batches hold one [MASK]
+// segment of ~12 % of all tokens: 7.9k rows at b128, 492 serial partial rows with fixed chunks).
+__device__ __forceinline__ int chunk_len(int len) {
+  const int r = (int)ceilf(sqrtf((float)len));
+  return r > kChunk ? r : kChunk;
+}
 
-template <typename T>
+// One WAVE per sorted position (4 per block), VEC-wide loads (16 B for bf16 rows with h % 8 ==
+// 0): positions that are not chunk leaders return at once, so a block-per-position grid spent
+// most of its time dispatching idle workgroups (~40 % of the step's non-GEMM "other" time).
+template <typename T, int VEC>
 __global__ void __launch_bounds__(256) embed_chunk_sum_kernel(const int64_t* __restrict__ perm,
                                                               const int64_t* __restrict__ seg_lo,
                                                               const int64_t* __restrict__ seg_hi,
                                                               const T* __restrict__ dz, float* __restrict__ scratch,
-                                                              int h) {
-  const int i = blockIdx.x;
-  const int lo = (int)seg_lo[i];
-  if ((i - lo) % kChunk) return;
-  const int end = min(i + kChunk, (int)seg_hi[i]);
-  for (int c = threadIdx.x * 2; c < h; c += blockDim.x * 2) {
-    float acc[2] = {0.f, 0.f};
+                                                              int rows, int h) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= rows) return;
+  const int lo = (int)seg_lo[i], shi = (int)seg_hi[i];
+  const int ch = chunk_len(shi - lo);
+  if ((i - lo) % ch) return;
+  const int end = min(i + ch, shi);
+  for (int c = lane * VEC; c < h; c += 64 * VEC) {
+    float acc[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
     for (int k = i; k < end; ++k) {
-      float x[2];
-      vload<T, 2>(dz + (size_t)perm[k] * h + c, x);
-      acc[0] += x[0]; acc[1] += x[1];
+      float x[VEC];
+      vload<T, VEC>(dz + (size_t)perm[k] * h + c, x);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += x[j];
     }
-    vstore<float, 2>(scratch + (size_t)i * h + c, acc);
+    vstore<float, VEC>(scratch + (size_t)i * h + c, acc);
   }
 }
 
-template <typename G>
+template <typename G, int VEC>
 __global__ void __launch_bounds__(256) embed_chunk_add_kernel(const int64_t* __restrict__ sorted_ids,
                                                               const int64_t* __restrict__ seg_lo,
                                                               const int64_t* __restrict__ seg_hi,
                                                               const float* __restrict__ scratch, G* __restrict__ grad,
-                                                              int h, int accumulate, int padding_idx) {
-  const int i = blockIdx.x;
-  if (seg_lo[i] != i) return;
+                                                              int rows, int h, int accumulate, int padding_idx) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= rows || seg_lo[i] != i) return;
   const int64_t id = sorted_ids[i];
   if (id == padding_idx) return;
   const int hi = (int)seg_hi[i];
+  const int ch = chunk_len(hi - i);
   G* g = grad + (size_t)id * h;
-  for (int c = threadIdx.x * 2; c < h; c += blockDim.x * 2) {
-    float acc[2] = {0.f, 0.f};
-    for (int k = i; k < hi; k += kChunk) {
-      float x[2];
-      vload<float, 2>(scratch + (size_t)k * h + c, x);
-      acc[0] += x[0]; acc[1] += x[1];
+  for (int c = lane * VEC; c < h; c += 64 * VEC) {
+    float acc[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+    for (int k = i; k < hi; k += ch) {
+      float x[VEC];
+      vload<float, VEC>(scratch + (size_t)k * h + c, x);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += x[j];
     }
     if (accumulate) {
-      float old[2];
-      vload<G, 2>(g + c, old);
-      acc[0] += old[0]; acc[1] += old[1];
+      float old[VEC];
+      vload<G, VEC>(g + c, old);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += old[j];
     }
-    vstore<G, 2>(g + c, acc);
+    vstore<G, VEC>(g + c, acc);
   }
 }
 
@@ -229,13 +249,21 @@ DTD_EXPORT int dtd_embed_word_bwd_chunked(int dtype, int grad_dtype, const int64
                                           const int64_t* seg_lo, const int64_t* seg_hi, float* scratch, const void* dz,
                                           void* grad, int rows, int h, int accumulate, int padding_idx, hipStream_t s) {
   if (rows <= 0) return 0;
-  if (dtype == kBF16)
-    hipLaunchKernelGGL(embed_chunk_sum_kernel<bf16>, dim3(rows), dim3(256), 0, s, perm, seg_lo, seg_hi, (const bf16*)dz, scratch, h);
-  else
-    hipLaunchKernelGGL(embed_chunk_sum_kernel<float>, dim3(rows), dim3(256), 0, s, perm, seg_lo, seg_hi, (const float*)dz, scratch, h);
-  if (grad_dtype == kBF16)
-    hipLaunchKernelGGL(embed_chunk_add_kernel<bf16>, dim3(rows), dim3(256), 0, s, sorted_ids, seg_lo, seg_hi, scratch, (bf16*)grad, h, accumulate, padding_idx);
-  else
-    hipLaunchKernelGGL(embed_chunk_add_kernel<float>, dim3(rows), dim3(256), 0, s, sorted_ids, seg_lo, seg_hi, scratch, (float*)grad, h, accumulate, padding_idx);
+  const dim3 grid((rows + 3) / 4);
+#define DTD_EMB_LAUNCH(V)                                                                                      \
+  if (dtype == kBF16)                                                                                          \
+    hipLaunchKernelGGL((embed_chunk_sum_kernel<bf16, V>), grid, dim3(256), 0, s, perm, seg_lo, seg_hi,         \
+                       (const bf16*)dz, scratch, rows, h);                                                     \
+  else                                                                                                         \
+    hipLaunchKernelGGL((embed_chunk_sum_kernel<float, V>), grid, dim3(256), 0, s, perm, seg_lo, seg_hi,        \
+                       (const float*)dz, scratch, rows, h);                                                    \
+  if (grad_dtype == kBF16)                                                                                     \
+    hipLaunchKernelGGL((embed_chunk_add_kernel<bf16, V>), grid, dim3(256), 0, s, sorted_ids, seg_lo, seg_hi,   \
+                       scratch, (bf16*)grad, rows, h, accumulate, padding_idx);                                \
+  else                                                                                                         \
+    hipLaunchKernelGGL((embed_chunk_add_kernel<float, V>), grid, dim3(256), 0, s, sorted_ids, seg_lo, seg_hi,  \
+                       scratch, (float*)grad, rows, h, accumulate, padding_idx)
+  if (h % 8 == 0) { DTD_EMB_LAUNCH(8); } else if (h % 2 == 0) { DTD_EMB_LAUNCH(2); } else { DTD_EMB_LAUNCH(1); }
+#undef DTD_EMB_LAUNCH
   DTD_LAUNCH_CHECK();
 }

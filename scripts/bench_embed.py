@@ -1,0 +1,44 @@
+#!/usr/bin/env python
+"""Word-embedding backward (sorted segment sum) at the BERT-base b128 shape, with its parts."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_training_and_deepspeed_amd.ops import functional as Fx  # noqa: E402
+
+
+def t_us(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+def main():
+    T, V, h = 65536, 28996, 768
+    ids = torch.randint(0, V, (T,), device="cuda")
+    if os.environ.get("SKEW", "1") == "1":   # synthetic MLM batches: ~12 % of tokens are [MASK]
+        ids[torch.rand(T, device="cuda") < 0.12] = 103
+    dz = torch.randn(T, h, device="cuda", dtype=torch.bfloat16)
+    g = torch.zeros(V, h, device="cuda", dtype=torch.bfloat16)
+    r = {}
+    r["word_bwd_total"] = t_us(lambda: Fx.embed_word_bwd(ids, dz, g, False, padding_idx=0))
+    r["sort"] = t_us(lambda: torch.sort(ids, stable=True))
+    s, perm = torch.sort(ids, stable=True)
+    r["searchsorted_x2"] = t_us(lambda: (torch.searchsorted(s, s, right=False), torch.searchsorted(s, s, right=True)))
+    r["zero_"] = t_us(lambda: g.zero_())
+    r["scratch_alloc"] = t_us(lambda: torch.empty((T, h), dtype=torch.float32, device="cuda"))
+    print(json.dumps({k: round(v, 1) for k, v in r.items()}))
+
+
+if __name__ == "__main__":
+    main()

@@ -148,6 +148,25 @@ def test_embedding_fwd_bwd():
         close(a, b, 2e-2)
 
 
+@pytest.mark.parametrize("acc,gdt", [(True, torch.float32), (False, torch.bfloat16)])
+def test_embedding_bwd_long_segments(acc, gdt):
+    """Skewed ids (one id repeated 1000x, a pad run): segments far longer than the 16-row chunks
+    of the sorted segment sum, bf16 and fp32 tables, overwrite and accumulate."""
+    torch.manual_seed(5)
+    V, h, n = 3000, 768, 4096
+    ids = torch.randint(0, V, (n,))
+    ids[:1000] = 7
+    ids[1000:1300] = 0
+    ids = ids[torch.randperm(n)]
+    dz = torch.randn(n, h, dtype=torch.bfloat16)
+    res = {}
+    for dev in (DEV, "cpu"):
+        g = torch.full((V, h), 0.25, dtype=gdt, device=dev)
+        Fx.embed_word_bwd(ids.to(dev), dz.to(dev), g, acc, padding_idx=0)
+        res[dev] = g.float().cpu()
+    close(res[DEV], res["cpu"], 2e-2)
+
+
 @pytest.mark.parametrize("hf", [False, True])
 def test_fused_adam_matches_reference(hf):
     from distributed_training_and_deepspeed_amd.optim.fused_adam import (MODE_ADAMW, MODE_BIAS_CORR, MODE_HF_EPS,
