@@ -21,9 +21,12 @@ struct GatherArgs {
   void* out; int rows, h, seq, pos_offset;
 };
 
-template <typename T>
+// One wave per output row (4 rows per block), VEC-wide (16-byte for bf16) loads of the word,
+// position and token-type rows.
+template <typename T, int VEC>
 __global__ void __launch_bounds__(256) embed_fwd_kernel(GatherArgs a) {
-  const int row = blockIdx.x;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= a.rows) return;
   const int64_t id = a.ids[row];
   const int pidx = (row % a.seq) + a.pos_offset;
   const int64_t tid = a.type_ids ? a.type_ids[row] : 0;
@@ -31,12 +34,20 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(GatherArgs a) {
   const T* p = a.pos ? (const T*)a.pos + (size_t)pidx * a.h : nullptr;
   const T* t = a.type ? (const T*)a.type + (size_t)tid * a.h : nullptr;
   T* o = (T*)a.out + (size_t)row * a.h;
-  for (int c = threadIdx.x * 2; c < a.h; c += blockDim.x * 2) {
-    float x[2], y[2];
-    vload<T, 2>(w + c, x);
-    if (p) { vload<T, 2>(p + c, y); x[0] += y[0]; x[1] += y[1]; }
-    if (t) { vload<T, 2>(t + c, y); x[0] += y[0]; x[1] += y[1]; }
-    vstore<T, 2>(o + c, x);
+  for (int c = lane * VEC; c < a.h; c += 64 * VEC) {
+    float x[VEC], y[VEC];
+    vload<T, VEC>(w + c, x);
+    if (p) {
+      vload<T, VEC>(p + c, y);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) x[j] += y[j];
+    }
+    if (t) {
+      vload<T, VEC>(t + c, y);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) x[j] += y[j];
+    }
+    vstore<T, VEC>(o + c, x);
   }
 }
 
@@ -144,25 +155,41 @@ __global__ void __launch_bounds__(256) embed_chunk_add_kernel(const int64_t* __r
   }
 }
 
-// grad_pos[s + offset] (+)= sum_b dz[b*seq + s]; grid = seq rows.
-template <typename T, typename G>
+// grad_pos[s + offset] (+)= sum_b dz[b*seq + s].  grid = (seq, ceil(h / (64*VEC))); the 4 waves
+// of a block split the batch rows (4 independent load chains instead of one serial one) and
+// combine in LDS in a fixed order (deterministic).
+template <typename T, typename G, int VEC>
 __global__ void __launch_bounds__(256) embed_pos_bwd_kernel(const T* __restrict__ dz, G* __restrict__ grad, int batch,
                                                             int seq, int h, int pos_offset, int accumulate) {
-  const int s = blockIdx.x;
-  G* g = grad + (size_t)(s + pos_offset) * h;
-  for (int c = threadIdx.x * 2; c < h; c += blockDim.x * 2) {
-    float acc[2] = {0.f, 0.f};
-    for (int b = 0; b < batch; ++b) {
-      float x[2];
-      vload<T, 2>(dz + ((size_t)b * seq + s) * h + c, x);
-      acc[0] += x[0]; acc[1] += x[1];
+  __shared__ float sh[4][64 * VEC];
+  const int s = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = (blockIdx.y * 64 + lane) * VEC;
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  if (c < h) {
+    for (int b = w; b < batch; b += 4) {
+      float x[VEC];
+      vload<T, VEC>(dz + ((size_t)b * seq + s) * h + c, x);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += x[j];
     }
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) sh[w][lane * VEC + j] = acc[j];
+  __syncthreads();
+  if (w == 0 && c < h) {
+    float tot[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) tot[j] = (sh[0][lane * VEC + j] + sh[1][lane * VEC + j]) + (sh[2][lane * VEC + j] + sh[3][lane * VEC + j]);
+    G* g = grad + (size_t)(s + pos_offset) * h + c;
     if (accumulate) {
-      float old[2];
-      vload<G, 2>(g + c, old);
-      acc[0] += old[0]; acc[1] += old[1];
+      float old[VEC];
+      vload<G, VEC>(g, old);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) tot[j] += old[j];
     }
-    vstore<G, 2>(g + c, acc);
+    vstore<G, VEC>(g, tot);
   }
 }
 
@@ -200,8 +227,14 @@ DTD_EXPORT int dtd_embed_fwd(int dtype, const int64_t* ids, const int64_t* type_
   if (rows <= 0) return 0;
   if (h % 2) return (int)hipErrorInvalidValue;
   GatherArgs a{ids, type_ids, word, pos, type, out, rows, h, seq, pos_offset};
-  if (dtype == kBF16) hipLaunchKernelGGL(embed_fwd_kernel<bf16>, dim3(rows), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(embed_fwd_kernel<float>, dim3(rows), dim3(256), 0, s, a);
+  const dim3 grid((rows + 3) / 4);
+  if (dtype == kBF16) {
+    if (h % 8 == 0) hipLaunchKernelGGL((embed_fwd_kernel<bf16, 8>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((embed_fwd_kernel<bf16, 2>), grid, dim3(256), 0, s, a);
+  } else {
+    if (h % 4 == 0) hipLaunchKernelGGL((embed_fwd_kernel<float, 4>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((embed_fwd_kernel<float, 2>), grid, dim3(256), 0, s, a);
+  }
   DTD_LAUNCH_CHECK();
 }
 
@@ -223,14 +256,17 @@ DTD_EXPORT int dtd_embed_word_bwd(int dtype, int grad_dtype, const int64_t* sort
 DTD_EXPORT int dtd_embed_pos_bwd(int dtype, int grad_dtype, const void* dz, void* grad, int batch, int seq, int h,
                                  int pos_offset, int accumulate, hipStream_t s) {
   if (batch <= 0) return 0;
-  if (dtype == kBF16 && grad_dtype == kBF16)
-    hipLaunchKernelGGL((embed_pos_bwd_kernel<bf16, bf16>), dim3(seq), dim3(256), 0, s, (const bf16*)dz, (bf16*)grad, batch, seq, h, pos_offset, accumulate);
-  else if (dtype == kBF16)
-    hipLaunchKernelGGL((embed_pos_bwd_kernel<bf16, float>), dim3(seq), dim3(256), 0, s, (const bf16*)dz, (float*)grad, batch, seq, h, pos_offset, accumulate);
-  else if (grad_dtype == kBF16)
-    hipLaunchKernelGGL((embed_pos_bwd_kernel<float, bf16>), dim3(seq), dim3(256), 0, s, (const float*)dz, (bf16*)grad, batch, seq, h, pos_offset, accumulate);
-  else
-    hipLaunchKernelGGL((embed_pos_bwd_kernel<float, float>), dim3(seq), dim3(256), 0, s, (const float*)dz, (float*)grad, batch, seq, h, pos_offset, accumulate);
+#define DTD_POS_BWD(T, G, V)                                                                              \
+  hipLaunchKernelGGL((embed_pos_bwd_kernel<T, G, V>), dim3(seq, (h + 64 * V - 1) / (64 * V)), dim3(256), 0, s, \
+                     (const T*)dz, (G*)grad, batch, seq, h, pos_offset, accumulate)
+#define DTD_POS_BWD_V(T, G) \
+  if (h % 8 == 0) { DTD_POS_BWD(T, G, 8); } else if (h % 2 == 0) { DTD_POS_BWD(T, G, 2); } else { DTD_POS_BWD(T, G, 1); }
+  if (dtype == kBF16 && grad_dtype == kBF16) { DTD_POS_BWD_V(bf16, bf16) }
+  else if (dtype == kBF16) { DTD_POS_BWD_V(bf16, float) }
+  else if (grad_dtype == kBF16) { DTD_POS_BWD_V(float, bf16) }
+  else { DTD_POS_BWD_V(float, float) }
+#undef DTD_POS_BWD_V
+#undef DTD_POS_BWD
   DTD_LAUNCH_CHECK();
 }
 
