@@ -46,6 +46,8 @@ def parse():
                     help="capture the whole training step in a hipGraph and replay it")
     ap.add_argument("--small-bucket-allreduce", default="rccl", choices=["rccl", "xgmi"],
                     help="xgmi: buckets <= 4 MiB use the native peer-mapped all-reduce kernel")
+    ap.add_argument("--async-wgrad", default="off", choices=["on", "off"],
+                    help="weight-gradient GEMMs on a side stream, concurrent with the dgrad chain")
     ap.add_argument("--dense-mlm-head", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
@@ -86,7 +88,8 @@ def main():
     model.rt.rng.reseed(1234 + rank)   # independent dropout masks per data-parallel replica
     gdt = {"bf16": torch.bfloat16, "fp32": torch.float32}.get(args.grad_dtype, dtype)
     ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt,
-                                  small_bucket_allreduce=args.small_bucket_allreduce)
+                                  small_bucket_allreduce=args.small_bucket_allreduce,
+                                  async_wgrad=args.async_wgrad == "on")
     opt = hf_adamw(ddp.parameters(), lr=5e-5)
 
     B, S = args.batch_size, args.seq_len
@@ -167,6 +170,7 @@ def main():
                 "optimizer": "fused AdamW (transformers.AdamW hyper-params, lr 5e-5)",
                 "tuned_gemms": tuned,
                 "hip_graph": graphed is not None,
+                "async_wgrad": args.async_wgrad == "on",
             },
             "loss_first": round(first_loss, 4),
             "loss_last": round(float(loss.detach()), 4),

@@ -282,9 +282,9 @@ class _FusedLayerFn(torch.autograd.Function):
         else:
             du = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1))
         grad_done(bf1)
-        emit_wgrad(w2, dy, a)
+        emit_wgrad(w2, dy, a, async_ok=True)
         del a
-        emit_wgrad(w1, du, f_in)
+        emit_wgrad(w1, du, f_in, async_ok=True)
         if c.pre_ln:
             dfin = du @ w1
             # z1 = x + dropout(o); f_in = LN2(z1); dz1 also receives dout (residual of out)
@@ -300,20 +300,20 @@ class _FusedLayerFn(torch.autograd.Function):
                                 dgamma=_acc(g1), dbeta=_acc(b1), dbias=_acc(o_b), dout2=dz2)
             for p in (g1, b1, o_b):
                 grad_done(p)
-        emit_wgrad(o_w, do, actx)
+        emit_wgrad(o_w, do, actx, async_ok=True)
         dctx = do @ o_w
         dqkv = A.attn_bwd(dctx, qkv, actx, lse, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, ctx.amask)
         Fx.bias_grad(dqkv, *_pair(qkv_b))
         grad_done(qkv_b)
         if c.pre_ln:
-            emit_wgrad(qkv_w, dqkv, a_in)
+            emit_wgrad(qkv_w, dqkv, a_in, async_ok=True)
             dain = dqkv @ qkv_w
             dx, _ = Fx.ln_bwd(dain, dz1, x2d, m1, r1, g1, 0.0, rng, 0, want_dz=True, want_dy=False,
                               dgamma=_acc(g1), dbeta=_acc(b1))
             for p in (g1, b1):
                 grad_done(p)
         else:
-            emit_wgrad(qkv_w, dqkv, x2d)
+            emit_wgrad(qkv_w, dqkv, x2d, async_ok=True)
             dx = dz1.addmm_(dqkv, qkv_w)   # in place: dz1 is this backward's own buffer (no C copy)
         return (dx.view(B, S, h), None) + (None,) * 12
 

@@ -110,8 +110,69 @@ def wgrad_splits(tokens: int, out_f: int, in_f: int) -> int:
     return s
 
 
-def emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
-    """p.grad-slot (+)= dy^T @ x for a Linear weight [out, in]; dy [T, out], x [T, in]."""
+class _AsyncWgrad:
+    """Side stream for weight-gradient GEMMs (opt-in, ``set_async_wgrad``).
+
+    In a layer's backward the wgrad GEMMs (compute-bound MFMA work) depend only on tensors the
+    dgrad chain has already produced, and nothing in the layer's backward reads their output.
+    Issued on a second HIP stream they run concurrently with the memory- / latency-bound
+    kernels of the dgrad chain (activation and LayerNorm backward, attention backward).  The
+    reducer joins the side stream (``join_async_wgrad``) before it reads gradients: before a
+    bucket's collective and before the optimizer."""
+
+    def __init__(self):
+        self.enabled = False
+        self.streams: dict = {}
+        self.pending = False
+
+    def stream(self, device) -> torch.cuda.Stream:
+        s = self.streams.get(device)
+        if s is None:
+            s = self.streams[device] = torch.cuda.Stream(device)
+        return s
+
+
+_ASYNC = _AsyncWgrad()
+
+
+def set_async_wgrad(enabled: bool) -> None:
+    _ASYNC.enabled = bool(enabled)
+
+
+def async_wgrad_enabled() -> bool:
+    return _ASYNC.enabled
+
+
+def join_async_wgrad(device=None) -> None:
+    """Make the current stream wait for every weight-gradient GEMM issued so far."""
+    if not _ASYNC.pending:
+        return
+    for dev, s in _ASYNC.streams.items():
+        if device is None or torch.device(device) == dev:
+            torch.cuda.current_stream(dev).wait_stream(s)
+    _ASYNC.pending = False
+
+
+def emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, async_ok: bool = False) -> None:
+    """p.grad-slot (+)= dy^T @ x for a Linear weight [out, in]; dy [T, out], x [T, in].
+    ``async_ok``: the caller guarantees that nothing else writes this parameter's gradient
+    before the reducer joins the side stream (per-layer Linear weights), so the GEMM may run
+    on the async-wgrad stream when that is enabled."""
+    if async_ok and _ASYNC.enabled and dy.is_cuda:
+        side = _ASYNC.stream(dy.device)
+        side.wait_stream(torch.cuda.current_stream(dy.device))
+        with torch.cuda.stream(side):
+            _emit_wgrad(p, dy, x)
+        dy.record_stream(side)      # keep the inputs alive for the side stream
+        x.record_stream(side)
+        _ASYNC.pending = True
+        grad_done(p)
+        return
+    _emit_wgrad(p, dy, x)
+    grad_done(p)
+
+
+def _emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
     dst, acc = grad_dst(p)
     T, o = dy.shape
     i = x.shape[1]
@@ -122,7 +183,6 @@ def emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
         a, b = dy.view(s, T // s, o).transpose(1, 2), x.view(s, T // s, i)
         part = _bmm_partials(a, b, fp32=dst.dtype == torch.float32)
         splitk_reduce(part, dst, acc)
-    grad_done(p)
 
 
 _F32_PARTIALS = [os.environ.get("DTD_WGRAD_F32_PARTIALS", "1") == "1"]

@@ -33,7 +33,13 @@ import torch.distributed as dist
 from torch import nn
 
 from ..comm import logger as comm_log
+from ..ops.grad import join_async_wgrad, set_async_wgrad
+from ..ops.grad import _ASYNC as _ASYNC_WGRAD
 from .flat import FlatLayout, GradBuffer
+
+
+def wgrad_stream(device) -> torch.cuda.Stream:
+    return _ASYNC_WGRAD.stream(device)
 
 
 class _Bucket:
@@ -60,7 +66,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, bucket_cap_mb: float = 25.0,
                  grad_dtype: torch.dtype | None = None, process_group=None, broadcast_parameters: bool = True,
                  overlap: bool = True, flatten_params: bool = True, small_bucket_allreduce: str = "rccl",
-                 xgmi_max_mb: float = 4.0):
+                 xgmi_max_mb: float = 4.0, async_wgrad: bool = False):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -86,6 +92,12 @@ class DistributedDataParallel(nn.Module):
             self._xgmi_stream = torch.cuda.Stream(self.device)
         elif small_bucket_allreduce not in ("rccl", "xgmi"):
             raise ValueError(f"small_bucket_allreduce must be 'rccl' or 'xgmi', got {small_bucket_allreduce!r}")
+        # weight-gradient GEMMs of the fused layers on a side stream (ops/grad.py _AsyncWgrad):
+        # bucket collectives are issued from that stream after it joins the compute stream, so
+        # neither stream blocks the other; finish() joins it before the optimizer reads grads
+        self.async_wgrad = bool(async_wgrad) and self.device.type == "cuda"
+        if self.async_wgrad:
+            set_async_wgrad(True)
         if broadcast_parameters and self.world > 1:
             self._broadcast_params()
 
@@ -165,11 +177,17 @@ class DistributedDataParallel(nn.Module):
             return
         view = self.grads.buf[b.start:b.end]
         if self._xgmi is not None and self._xgmi.supports(view):
+            join_async_wgrad(self.device)
             side = self._xgmi_stream
             side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(side):
                 self._xgmi.all_reduce(view, average=True)
             b.work = _StreamWork(side, self.device)
+        elif self.backend == "nccl" and self.async_wgrad:
+            side = wgrad_stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))   # bias / LN grads of the bucket
+            with torch.cuda.stream(side):
+                b.work = comm_log.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
         elif self.backend == "nccl":
             b.work = comm_log.all_reduce(view, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
         else:
@@ -183,6 +201,8 @@ class DistributedDataParallel(nn.Module):
     def finish(self) -> None:
         """Launch any bucket not yet launched (unused parameters get zero gradients) and make
         the current stream wait for every all-reduce."""
+        if self.async_wgrad:
+            join_async_wgrad(self.device)
         self.grads.zero_untouched_()
         for b in self.buckets:
             if not b.launched:
