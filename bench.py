@@ -144,7 +144,8 @@ def main():
     value = tokens / dt
     if rank == 0:
         res = {
-            "metric": "tokens/sec (whole node) BERT-base DDP",
+            "metric": "tokens/sec (whole node) BERT-base DDP" if cfg.name == "bert-base-cased"
+                      else f"tokens/sec (whole node) {cfg.name} DDP",
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": world,
