@@ -108,3 +108,25 @@ def test_ddp_two_ranks_share_one_gpu_stay_in_sync(tmp_path, free_port):
     a = torch.load(tmp_path / "p0.pt", weights_only=True)
     b = torch.load(tmp_path / "p1.pt", weights_only=True)
     assert torch.equal(a, b)
+
+
+def test_rccl_bf16_avg_collectives_used_by_ddp_and_zero(rccl_world1):
+    """The exact RCCL calls the DDP / ZeRO reducers issue (bf16 AVG all-reduce from a side stream,
+    reduce-scatter, all-gather) are accepted by this torch+RCCL build (world 1 on one GPU)."""
+    import torch.distributed as dist
+    from distributed_training_and_deepspeed_amd.comm import logger as clog
+    x = torch.randn(1 << 20, device="cuda").bfloat16()
+    ref = x.clone()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        w = clog.all_reduce(x, op=dist.ReduceOp.AVG, async_op=True)
+    w.wait()
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
+    out = torch.empty_like(x)
+    clog.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG, async_op=False)
+    gat = torch.empty_like(x)
+    clog.all_gather_into_tensor(gat, out, async_op=False)
+    torch.cuda.synchronize()
+    assert torch.equal(gat, ref)
