@@ -16,8 +16,10 @@ Results are bitwise identical on every rank (fixed summation order).  Messages a
 single-process variant (``world`` virtual ranks on one GPU) used by the tests on a 1-GPU box.
 
 Status: the kernel logic, the barrier protocol and the epoch double-buffering are tested in
-local mode on one MI355X; the IPC (multi-GPU) path needs an 8-GPU node and is opt-in
-(``DistributedDataParallel(small_bucket_allreduce="xgmi")``).
+local mode on one MI355X, and the IPC path (handle exchange, ``hipIpcOpenMemHandle`` mapping,
+cross-process release/acquire barrier) with 2 and 4 processes sharing one MI355X
+(``tests/test_xgmi_gpu.py::test_ipc_mode_processes_share_one_gpu``).  Cross-GPU xGMI traffic
+needs a multi-GPU node; the path is opt-in (``DistributedDataParallel(small_bucket_allreduce="xgmi")``).
 """
 from __future__ import annotations
 

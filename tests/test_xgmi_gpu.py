@@ -44,3 +44,41 @@ def test_local_allreduce_average_and_many_epochs():
         assert not ar.error()
     finally:
         ar.close()
+
+
+def _ipc_rank(rank, world, port, out):
+    """Real (IPC) mode: `world` processes on the same GPU map each other's staging and signal buffers
+    through hipIpcOpenMemHandle, exactly as ranks on different GPUs of a node do."""
+    from distributed_training_and_deepspeed_amd import comm
+    comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
+    torch.cuda.set_device(0)
+    ar = XgmiAllReduce(max_bytes=4 << 20, one_shot_max=64 << 10, blocks=8)
+    ok = True
+    try:
+        for dtype in (torch.bfloat16, torch.float32):
+            for it, numel in enumerate([8 * world * 3, 16384, 1 << 19]):   # one-shot, one-shot, two-shot
+                g = torch.Generator().manual_seed(1000 * it + 7)
+                xs = [torch.randn(numel, generator=g).to(dtype) for _ in range(world)]
+                ref = xs[0].float().clone()
+                for x in xs[1:]:
+                    ref += x.float()
+                mine = xs[rank].cuda()
+                ar.all_reduce(mine, average=(it == 1))
+                torch.cuda.synchronize()
+                want = (ref / world if it == 1 else ref).to(dtype)
+                ok &= torch.equal(mine.cpu(), want)
+        ok &= not ar.error()
+    finally:
+        torch.distributed.barrier()
+        ar.close()
+        torch.distributed.barrier()
+    with open(f"{out}/r{rank}", "w") as f:
+        f.write("ok" if ok else "bad")
+    comm.destroy()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_mode_processes_share_one_gpu(tmp_path, free_port, world):
+    import torch.multiprocessing as mp
+    mp.spawn(_ipc_rank, args=(world, free_port, str(tmp_path)), nprocs=world, join=True)
+    assert [(tmp_path / f"r{r}").read_text() for r in range(world)] == ["ok"] * world
