@@ -14,6 +14,10 @@ draws its own dropout masks (seed offset by rank).
   python bench.py --gpus N --steps K --warmup W
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+Other BASELINE configs through the same timing contract: ``--model large`` (BERT-large DDP),
+``--zero-stage 2`` (BERT-base through the ZeRO engine of zero_dp_training.py), ``--model
+gpt2-medium --zero-stage 3``.
+
 Rank 0 prints ONE JSON line; ``value`` = total tokens/s over all ranks, computed from the
 MAX step time over ranks.
 """
@@ -48,6 +52,10 @@ def parse():
                     help="xgmi: buckets <= 4 MiB use the native peer-mapped all-reduce kernel")
     ap.add_argument("--async-wgrad", default="off", choices=["on", "off"],
                     help="weight-gradient GEMMs on a side stream, concurrent with the dgrad chain")
+    ap.add_argument("--zero-stage", type=int, default=None, choices=[0, 1, 2, 3],
+                    help="train through the ZeRO engine (zero_dp_training.py's path) instead of DDP")
+    ap.add_argument("--reduce-bucket", type=float, default=2.5e7,
+                    help="ZeRO reduce_bucket_size (elements) for --zero-stage")
     ap.add_argument("--dense-mlm-head", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
@@ -76,21 +84,33 @@ def main():
             from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
             tuned = use_tuned_gemms()
     device = torch.device("cuda", local) if cuda else torch.device("cpu")
-    if world > 1:
+    if world > 1 or args.zero_stage is not None:   # the ZeRO engine always runs on a process group
         comm.init(rank=rank, world_size=world, local_rank=local)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     cfg = get_config(args.model)
+    mlm = cfg.family == "bert"
     model = build_model(args.model, impl=args.impl, dtype=dtype, device=device, seed=1234,
-                        sparse_mlm_head=not args.dense_mlm_head)
+                        **({"sparse_mlm_head": not args.dense_mlm_head} if mlm else {}))
     if args.impl == "reference":
         model.rt.exact_dropout = False  # torch-eager baseline: ATen dropout, HF-style eager ops
     model.train()
     model.rt.rng.reseed(1234 + rank)   # independent dropout masks per data-parallel replica
     gdt = {"bf16": torch.bfloat16, "fp32": torch.float32}.get(args.grad_dtype, dtype)
-    ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt,
-                                  small_bucket_allreduce=args.small_bucket_allreduce,
-                                  async_wgrad=args.async_wgrad == "on")
-    opt = hf_adamw(ddp.parameters(), lr=5e-5)
+    zero = args.zero_stage is not None
+    if zero:
+        from distributed_training_and_deepspeed_amd.parallel.zero import initialize
+        # zero_dp_training.py's DeepSpeed config (Adam lr 1.5e-4), larger reduce buckets
+        zcfg = {"train_micro_batch_size_per_gpu": args.batch_size,
+                "optimizer": {"type": "Adam", "params": {"lr": 1.5e-4}},
+                "zero_optimization": {"stage": args.zero_stage, "reduce_bucket_size": args.reduce_bucket},
+                "bf16": {"enabled": dtype == torch.bfloat16}}
+        engine, _, _, _ = initialize(model=model, model_parameters=model.parameters(), config=zcfg)
+        gdt = engine.grad_dtype
+    else:
+        ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt,
+                                      small_bucket_allreduce=args.small_bucket_allreduce,
+                                      async_wgrad=args.async_wgrad == "on")
+        opt = hf_adamw(ddp.parameters(), lr=5e-5)
 
     B, S = args.batch_size, args.seq_len
     nb = args.warmup + args.steps
@@ -100,6 +120,11 @@ def main():
     nbuf = ids.shape[0]
 
     def train_step(input_ids, labels):
+        if zero:
+            out = engine(input_ids, labels=labels)
+            engine.backward(out.loss)
+            engine.step()                # advances the dropout RNG step itself
+            return out.loss.detach()
         out = ddp(input_ids, labels=labels)
         out.loss.backward()
         opt.step()
@@ -107,7 +132,7 @@ def main():
         return out.loss.detach()
 
     graphed = None
-    if args.graph == "on" and cuda:
+    if args.graph == "on" and cuda and not zero:
         # one hipGraph replay per step (host-launch-bound small batches); static-size MLM head
         from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep, mlm_capacity
         model.rt.mlm_capacity = mlm_capacity(B * S)
@@ -143,9 +168,10 @@ def main():
     tokens = world * B * S * args.steps
     value = tokens / dt
     if rank == 0:
+        engine_name = f"ZeRO-{args.zero_stage}" if zero else "DDP"
         res = {
-            "metric": "tokens/sec (whole node) BERT-base DDP" if cfg.name == "bert-base-cased"
-                      else f"tokens/sec (whole node) {cfg.name} DDP",
+            "metric": "tokens/sec (whole node) BERT-base DDP" if cfg.name == "bert-base-cased" and not zero
+                      else f"tokens/sec (whole node) {cfg.name} {engine_name}",
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -156,19 +182,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic (random token ids, HF MLM 15%/80/10/10 masking; random-init weights)",
+            "data": ("synthetic (random token ids, HF MLM 15%/80/10/10 masking; random-init weights)" if mlm
+                     else "synthetic (random token ids, causal labels = input_ids; random-init weights)"),
             "config": {
                 "model": cfg.name,
                 "params": sum(p.numel() for p in model.parameters()),
                 "global_batch": B * world,
                 "per_gpu_batch": B,
                 "seq_len": S,
-                "parallelism": f"dp{world}",
-                "bucket_mb": args.bucket_mb,
+                "parallelism": f"zero{args.zero_stage}-dp{world}" if zero else f"dp{world}",
+                "bucket_mb": args.reduce_bucket * 2 / 2 ** 20 if zero else args.bucket_mb,
                 "grad_dtype": str(gdt).replace("torch.", ""),
                 "impl": args.impl,
-                "mlm_head": "dense" if args.dense_mlm_head else "sparse (labelled rows only; identical loss/grads)",
-                "optimizer": "fused AdamW (transformers.AdamW hyper-params, lr 5e-5)",
+                "mlm_head": (None if not mlm else "dense" if args.dense_mlm_head
+                             else "sparse (labelled rows only; identical loss/grads)"),
+                "optimizer": ("fused Adam on the ZeRO shard (zero_dp_training.py config, lr 1.5e-4)" if zero
+                              else "fused AdamW (transformers.AdamW hyper-params, lr 5e-5)"),
                 "tuned_gemms": tuned,
                 "hip_graph": graphed is not None,
                 "async_wgrad": args.async_wgrad == "on",
@@ -177,7 +206,7 @@ def main():
             "loss_last": round(float(loss.detach()), 4),
         }
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if world > 1 or zero:
         comm.destroy()
 
 

@@ -323,8 +323,6 @@ class ZeroEngine(nn.Module):
             p._dtd_touched = False
 
     def _on_ready(self, p, autograd: bool = False) -> None:
-        if not self._callback_queued and torch.is_grad_enabled() is False:
-            pass
         if not self._callback_queued:
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
@@ -550,7 +548,9 @@ class ZeroEngine(nn.Module):
         bucket from the updated shards; stage 3 units stay sharded until their next use."""
         if self.stage == 0:
             for s in self.buckets:
-                s.full.copy_(self.lowp_view[s.shard_off:s.shard_off + s.chunk])
+                src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
+                if src.data_ptr() != s.full.data_ptr():   # aliased (the usual case): nothing to copy
+                    s.full.copy_(src)
             return
         for s in self.buckets:
             src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
