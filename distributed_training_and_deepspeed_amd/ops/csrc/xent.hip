@@ -6,18 +6,29 @@
 //   forward : one read of each row -> per-row loss and log-sum-exp (online max/sum in fp32)
 //   reduce  : one block -> mean loss over valid rows + valid count (device scalars; no host sync)
 //   backward: one read + one write -> dlogits = (softmax - onehot) * grad_out / count
-// One 256-thread workgroup per row; rows are read with the widest vector (8/4/2/1 elements)
-// that divides V, so odd vocabularies (GPT-2, 50257) stay correct.
+// One 256-thread workgroup per row.  Rows are read with 16-byte vectors whatever V is: a row of
+// an odd vocabulary (GPT-2, 50257) starts at any 2-byte boundary, so each row is split into a
+// scalar head up to the next 16-byte boundary, an aligned 16-byte body and a scalar tail (the
+// first version fell back to 2-byte loads for odd V and ran at ~1.8 TB/s).
 #include "common.h"
 
 using namespace dtd;
 
 namespace {
 
+// [0, head) scalar, [head, body) 16-byte vectors of VEC elements, [body, V) scalar.
 template <typename T, int VEC>
+__device__ __forceinline__ void row_split(const T* z, int V, int& head, int& body) {
+  const int mis = (int)((reinterpret_cast<uintptr_t>(z) & 15) / sizeof(T));
+  head = mis ? min(V, VEC - mis) : 0;
+  body = head + (V - head) / VEC * VEC;
+}
+
+template <typename T>
 __global__ void __launch_bounds__(256) xent_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ labels,
                                                        float* __restrict__ loss_row, float* __restrict__ lse_row,
                                                        int rows, int V, int ignore_index) {
+  constexpr int VEC = 16 / sizeof(T);
   __shared__ float sh[8];
   const int row = blockIdx.x;
   const int64_t y = labels[row];
@@ -26,8 +37,16 @@ __global__ void __launch_bounds__(256) xent_fwd_kernel(const T* __restrict__ log
     return;
   }
   const T* z = logits + (size_t)row * V;
+  int head, body;
+  row_split<T, VEC>(z, V, head, body);
   float m = -INFINITY, s = 0.f;
-  for (int c = threadIdx.x * VEC; c < V; c += blockDim.x * VEC) {
+  auto add1 = [&](float t) {
+    if (t > m) { s *= __expf(m - t); m = t; }
+    s += __expf(t - m);
+  };
+  if ((int)threadIdx.x < head) add1((float)z[threadIdx.x]);
+#pragma unroll 2
+  for (int c = head + threadIdx.x * VEC; c < body; c += blockDim.x * VEC) {
     float t[VEC];
     vload<T, VEC>(z + c, t);
     float lm = t[0];
@@ -37,6 +56,7 @@ __global__ void __launch_bounds__(256) xent_fwd_kernel(const T* __restrict__ log
 #pragma unroll
     for (int j = 0; j < VEC; ++j) s += __expf(t[j] - m);
   }
+  for (int c = body + threadIdx.x; c < V; c += blockDim.x) add1((float)z[c]);
   const float M = block_max(m, sh);
   s = (m == -INFINITY) ? 0.f : s * __expf(m - M);
   const float S = block_sum(s, sh);
@@ -61,57 +81,46 @@ __global__ void __launch_bounds__(256) xent_reduce_kernel(const float* __restric
   if (threadIdx.x == 0) { out[0] = c > 0.f ? s / c : NAN; out[1] = c; }
 }
 
-template <typename T, int VEC>
+// logits and dlogits share their 16-byte phase (checked on the host), so one split serves both.
+template <typename T>
 __global__ void __launch_bounds__(256) xent_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ labels,
                                                        const float* __restrict__ lse_row, const float* __restrict__ stats,
                                                        const float* __restrict__ grad_out, T* __restrict__ dlogits,
                                                        int rows, int V, int ignore_index) {
+  constexpr int VEC = 16 / sizeof(T);
   const int row = blockIdx.x;
   const int64_t y = labels[row];
-  T* dz = dlogits + (size_t)row * V;
-  if (y == ignore_index) {
-    float zero[VEC];
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) zero[j] = 0.f;
-    for (int c = threadIdx.x * VEC; c < V; c += blockDim.x * VEC) vstore<T, VEC>(dz + c, zero);
-    return;
-  }
-  const float g = grad_out[0] / stats[1];
-  const float lse = lse_row[row];
   const T* z = logits + (size_t)row * V;
-  for (int c = threadIdx.x * VEC; c < V; c += blockDim.x * VEC) {
+  T* dz = dlogits + (size_t)row * V;
+  int head, body;
+  row_split<T, VEC>(z, V, head, body);
+  const bool ign = y == ignore_index;   // uniform per block: the row's gradient is zero
+  const float g = ign ? 0.f : grad_out[0] / stats[1];
+  const float lse = ign ? 0.f : lse_row[row];
+  auto grad1 = [&](int c) {
+    float p = ign ? 0.f : __expf((float)z[c] - lse);
+    if (c == y) p -= 1.f;
+    dz[c] = (T)(p * g);
+  };
+  if ((int)threadIdx.x < head) grad1(threadIdx.x);
+#pragma unroll 2
+  for (int c = head + threadIdx.x * VEC; c < body; c += blockDim.x * VEC) {
     float t[VEC];
-    vload<T, VEC>(z + c, t);
+    if (ign) {
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      float p = __expf(t[j] - lse);
-      if (c + j == y) p -= 1.f;
-      t[j] = p * g;
+      for (int j = 0; j < VEC; ++j) t[j] = 0.f;
+    } else {
+      vload<T, VEC>(z + c, t);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        float p = __expf(t[j] - lse);
+        if (c + j == y) p -= 1.f;
+        t[j] = p * g;
+      }
     }
     vstore<T, VEC>(dz + c, t);
   }
-}
-
-template <typename T>
-int launch_fwd(const void* logits, const int64_t* labels, float* loss_row, float* lse_row, int rows, int V, int ign,
-               hipStream_t s) {
-  const T* z = (const T*)logits;
-  if (V % 8 == 0) hipLaunchKernelGGL((xent_fwd_kernel<T, 8>), dim3(rows), dim3(256), 0, s, z, labels, loss_row, lse_row, rows, V, ign);
-  else if (V % 4 == 0) hipLaunchKernelGGL((xent_fwd_kernel<T, 4>), dim3(rows), dim3(256), 0, s, z, labels, loss_row, lse_row, rows, V, ign);
-  else if (V % 2 == 0) hipLaunchKernelGGL((xent_fwd_kernel<T, 2>), dim3(rows), dim3(256), 0, s, z, labels, loss_row, lse_row, rows, V, ign);
-  else hipLaunchKernelGGL((xent_fwd_kernel<T, 1>), dim3(rows), dim3(256), 0, s, z, labels, loss_row, lse_row, rows, V, ign);
-  return 0;
-}
-template <typename T>
-int launch_bwd(const void* logits, const int64_t* labels, const float* lse_row, const float* stats, const float* gout,
-               void* dlogits, int rows, int V, int ign, hipStream_t s) {
-  const T* z = (const T*)logits;
-  T* d = (T*)dlogits;
-  if (V % 8 == 0) hipLaunchKernelGGL((xent_bwd_kernel<T, 8>), dim3(rows), dim3(256), 0, s, z, labels, lse_row, stats, gout, d, rows, V, ign);
-  else if (V % 4 == 0) hipLaunchKernelGGL((xent_bwd_kernel<T, 4>), dim3(rows), dim3(256), 0, s, z, labels, lse_row, stats, gout, d, rows, V, ign);
-  else if (V % 2 == 0) hipLaunchKernelGGL((xent_bwd_kernel<T, 2>), dim3(rows), dim3(256), 0, s, z, labels, lse_row, stats, gout, d, rows, V, ign);
-  else hipLaunchKernelGGL((xent_bwd_kernel<T, 1>), dim3(rows), dim3(256), 0, s, z, labels, lse_row, stats, gout, d, rows, V, ign);
-  return 0;
+  for (int c = body + threadIdx.x; c < V; c += blockDim.x) grad1(c);
 }
 
 }  // namespace
@@ -119,8 +128,12 @@ int launch_bwd(const void* logits, const int64_t* labels, const float* lse_row, 
 DTD_EXPORT int dtd_xent_fwd(int dtype, const void* logits, const int64_t* labels, float* loss_row, float* lse_row,
                             float* stats, int rows, int V, int ignore_index, hipStream_t s) {
   if (rows <= 0) return 0;
-  if (dtype == kBF16) launch_fwd<bf16>(logits, labels, loss_row, lse_row, rows, V, ignore_index, s);
-  else launch_fwd<float>(logits, labels, loss_row, lse_row, rows, V, ignore_index, s);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(xent_fwd_kernel<bf16>, dim3(rows), dim3(256), 0, s, (const bf16*)logits, labels, loss_row,
+                       lse_row, rows, V, ignore_index);
+  else
+    hipLaunchKernelGGL(xent_fwd_kernel<float>, dim3(rows), dim3(256), 0, s, (const float*)logits, labels, loss_row,
+                       lse_row, rows, V, ignore_index);
   hipLaunchKernelGGL(xent_reduce_kernel, dim3(1), dim3(256), 0, s, loss_row, labels, rows, ignore_index, stats);
   DTD_LAUNCH_CHECK();
 }
@@ -129,7 +142,12 @@ DTD_EXPORT int dtd_xent_bwd(int dtype, const void* logits, const int64_t* labels
                             const float* stats, const float* grad_out, void* dlogits, int rows, int V,
                             int ignore_index, hipStream_t s) {
   if (rows <= 0) return 0;
-  if (dtype == kBF16) launch_bwd<bf16>(logits, labels, lse_row, stats, grad_out, dlogits, rows, V, ignore_index, s);
-  else launch_bwd<float>(logits, labels, lse_row, stats, grad_out, dlogits, rows, V, ignore_index, s);
+  if ((reinterpret_cast<uintptr_t>(logits) & 15) != (reinterpret_cast<uintptr_t>(dlogits) & 15)) return -1;
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(xent_bwd_kernel<bf16>, dim3(rows), dim3(256), 0, s, (const bf16*)logits, labels, lse_row,
+                       stats, grad_out, (bf16*)dlogits, rows, V, ignore_index);
+  else
+    hipLaunchKernelGGL(xent_bwd_kernel<float>, dim3(rows), dim3(256), 0, s, (const float*)logits, labels, lse_row,
+                       stats, grad_out, (float*)dlogits, rows, V, ignore_index);
   DTD_LAUNCH_CHECK();
 }

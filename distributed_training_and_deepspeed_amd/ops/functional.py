@@ -271,7 +271,13 @@ def xent_bwd(logits, labels, lse, stats, grad_out, ignore_index: int = IGNORE_IN
         p[torch.arange(rows), labels.clamp_min(0)] -= 1.0
         p = p * valid[:, None].float() * (grad_out.float() / stats[1])
         return p.to(logits.dtype).view_as(logits)
-    d = torch.empty_like(logits)
+    phase = logits.data_ptr() % 16   # the kernel needs dlogits in the same 16-byte phase
+    if phase:
+        es = logits.element_size()
+        buf = torch.empty(logits.numel() + 16 // es, dtype=logits.dtype, device=logits.device)
+        d = buf[phase // es:phase // es + logits.numel()].view_as(logits)
+    else:
+        d = torch.empty_like(logits)
     gout = grad_out.reshape(1).to(torch.float32).contiguous()
     _lib.call("dtd_xent_bwd", _lib.dt(logits), logits.data_ptr(), labels.contiguous().to(torch.int64).data_ptr(),
               lse.data_ptr(), stats.data_ptr(), gout.data_ptr(), d.data_ptr(), rows, V, ignore_index,

@@ -107,18 +107,24 @@ def test_activation_fast_math_accuracy_fp32(act):
     assert (g - gr).abs().max().item() < 2e-6
 
 
-@pytest.mark.parametrize("V", [28996, 50257, 1000, 250880])
-def test_softmax_xent(V):
+@pytest.mark.parametrize("V,dtype,offset", [(28996, torch.bfloat16, 0), (50257, torch.bfloat16, 0), (1000, torch.bfloat16, 0),
+                                            (250880, torch.bfloat16, 0), (7, torch.bfloat16, 0), (50257, torch.bfloat16, 3),
+                                            (50257, torch.float32, 1), (13, torch.float32, 0)])
+def test_softmax_xent(V, dtype, offset):
+    """Odd vocabularies / unaligned bases: every row mixes a scalar head, 16-byte body and tail."""
     torch.manual_seed(2)
     rows = 64
-    z = (3 * torch.randn(rows, V)).to(torch.bfloat16)
+    z = (3 * torch.randn(rows * V + offset))[offset:].view(rows, V).to(dtype)
     lab = torch.randint(0, V, (rows,))
     lab[::3] = -100
     gout = torch.tensor(0.7)
     res = {}
     for dev in (DEV, "cpu"):
-        loss, lse, st = Fx.xent_fwd(z.to(dev), lab.to(dev))
-        d = Fx.xent_bwd(z.to(dev), lab.to(dev), lse, st, gout.to(dev))
+        zd = z.to(dev)
+        if offset and dev == DEV:   # an unaligned device view
+            zd = torch.empty(rows * V + offset, dtype=dtype, device=dev)[offset:].view(rows, V).copy_(zd)
+        loss, lse, st = Fx.xent_fwd(zd, lab.to(dev))
+        d = Fx.xent_bwd(zd, lab.to(dev), lse, st, gout.to(dev))
         res[dev] = (loss, lse, st, d)
     ref = torch.nn.functional.cross_entropy(z.float(), lab, ignore_index=-100)
     close(res[DEV][0], ref, 1e-4)
