@@ -238,7 +238,7 @@ class _FusedLayerFn(torch.autograd.Function):
         a = Fx.act_fwd(u, c.activation)
         y = F.linear(a, w2, bf2)
         if c.pre_ln:
-            out = z1 + Fx.dropout(y, p_h, rng, s2)
+            out = Fx.dropout_add(y, z1, p_h, rng, s2)
             z2 = m3 = r3 = None
         else:
             z2, out, m3, r3 = Fx.ln_fwd(y, f_in, g2, b2, eps, p_h, rng, s2)

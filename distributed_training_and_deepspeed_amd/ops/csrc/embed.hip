@@ -194,7 +194,10 @@ __global__ void __launch_bounds__(256) embed_pos_bwd_kernel(const T* __restrict_
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) dropout_kernel(const T* __restrict__ x, T* __restrict__ y, size_t n, float p,
+// y = dropout(x), or y = res + dropout(x) with the sum in fp32 (pre-LN residual branch: one pass
+// instead of a dropout pass + an add pass)
+__global__ void __launch_bounds__(256) dropout_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                      T* __restrict__ y, size_t n, float p,
                                                       const uint64_t* rng, uint32_t stream_id) {
   DropoutRng g(rng, stream_id);
   const uint32_t thr = keep_threshold(p);
@@ -209,13 +212,19 @@ __global__ void __launch_bounds__(256) dropout_kernel(const T* __restrict__ x, T
       t[j] *= ((b & 0xffffu) >= thr) ? scale : 0.f;
       t[j + 1] *= ((b >> 16) >= thr) ? scale : 0.f;
     }
+    if (res) {
+      float u[8];
+      vload<T, 8>(res + i * 8, u);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] += u[j];
+    }
     vstore<T, 8>(y + i * 8, t);
   }
   if (blockIdx.x == 0) {
     for (size_t e = nv * 8 + threadIdx.x; e < n; e += blockDim.x) {
       const uint32_t b = g.bits(e >> 1);
       const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
-      y[e] = (T)((float)x[e] * (h16 >= thr ? scale : 0.f));
+      y[e] = (T)((float)x[e] * (h16 >= thr ? scale : 0.f) + (res ? (float)res[e] : 0.f));
     }
   }
 }
@@ -270,14 +279,19 @@ DTD_EXPORT int dtd_embed_pos_bwd(int dtype, int grad_dtype, const void* dz, void
   DTD_LAUNCH_CHECK();
 }
 
-DTD_EXPORT int dtd_dropout(int dtype, const void* x, void* y, size_t n, float p, const uint64_t* rng,
+// y = dropout(x) (res == nullptr) or y = res + dropout(x)
+DTD_EXPORT int dtd_dropout(int dtype, const void* x, const void* res, void* y, size_t n, float p, const uint64_t* rng,
                            uint32_t stream_id, hipStream_t s) {
   if (n == 0) return 0;
   size_t blocks = (n / 8 + 255) / 256;
   if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;
-  if (dtype == kBF16) hipLaunchKernelGGL(dropout_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, (bf16*)y, n, p, rng, stream_id);
-  else hipLaunchKernelGGL(dropout_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, (float*)y, n, p, rng, stream_id);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(dropout_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, (const bf16*)res, (bf16*)y, n,
+                       p, rng, stream_id);
+  else
+    hipLaunchKernelGGL(dropout_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, (const float*)res,
+                       (float*)y, n, p, rng, stream_id);
   DTD_LAUNCH_CHECK();
 }
 

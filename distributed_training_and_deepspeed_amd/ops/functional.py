@@ -43,7 +43,19 @@ def dropout(x: torch.Tensor, p: float, rng: RngState, sid: int) -> torch.Tensor:
         return _ref_dropout(x, p, rng, sid)
     x = x.contiguous()
     y = torch.empty_like(x)
-    _lib.call("dtd_dropout", _lib.dt(x), x.data_ptr(), y.data_ptr(), x.numel(), float(p),
+    _lib.call("dtd_dropout", _lib.dt(x), x.data_ptr(), None, y.data_ptr(), x.numel(), float(p),
+              rng.state.data_ptr(), sid, _lib.stream())
+    return y
+
+
+def dropout_add(x: torch.Tensor, res: torch.Tensor, p: float, rng: RngState, sid: int) -> torch.Tensor:
+    """res + dropout(x) in one pass (sum in fp32); same keep bits as ``dropout(x, p, rng, sid)``."""
+    if not _on_gpu(x):
+        return res + dropout(x, p, rng, sid)
+    assert x.shape == res.shape and x.dtype == res.dtype
+    x, res = x.contiguous(), res.contiguous()
+    y = torch.empty_like(x)
+    _lib.call("dtd_dropout", _lib.dt(x), x.data_ptr(), res.data_ptr(), y.data_ptr(), x.numel(), float(p),
               rng.state.data_ptr(), sid, _lib.stream())
     return y
 

@@ -46,6 +46,21 @@ def test_dropout_mask_matches_reference(dtype):
     assert abs(frac - 0.9) < 0.002
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_dropout_add_fused_residual(dtype):
+    """res + dropout(x) in one pass: same keep bits as dropout(), sum taken in fp32."""
+    g, c = rng_pair()
+    n = 1000003   # odd: the scalar tail path
+    x = torch.randn(n, dtype=dtype, device=DEV)
+    res = torch.randn(n, dtype=dtype, device=DEV)
+    y = Fx.dropout_add(x, res, 0.1, g, 78)
+    keep = keep_mask(n, 0.1, 7, 3, 78).to(DEV)
+    ref = (res.float() + x.float() * keep.float() / 0.9).to(dtype)
+    close(y, ref, 1e-2 if dtype == torch.bfloat16 else 1e-6)
+    z = Fx.dropout_add(x, res, 0.0, g, 78)      # eval: plain residual add
+    close(z, (res.float() + x.float()).to(dtype), 1e-2 if dtype == torch.bfloat16 else 1e-6)
+
+
 @pytest.mark.parametrize("h", [128, 768, 1024, 1280, 384, 2304])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_layernorm_fwd_bwd(h, dtype):
