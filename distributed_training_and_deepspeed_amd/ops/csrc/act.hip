@@ -76,15 +76,15 @@ __device__ __forceinline__ void act_fdf(float x, float& y, float& dy) {
   }
 }
 
-template <typename T, int ACT>
+template <typename T, int ACT, int NT>
 __global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ u, T* __restrict__ y, size_t n) {
   const size_t nv = n / 8;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
     float t[8];
-    vload<T, 8>(u + i * 8, t);
+    if (NT & 1) vload_nt<T, 8>(u + i * 8, t); else vload<T, 8>(u + i * 8, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) t[j] = act_f<ACT>(t[j]);
-    vstore<T, 8>(y + i * 8, t);
+    if (NT & 2) vstore_nt<T, 8>(y + i * 8, t); else vstore<T, 8>(y + i * 8, t);
   }
   // tail (n % 8) handled by block 0
   if (blockIdx.x == 0) {
@@ -98,11 +98,13 @@ __global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ u, T
 // grid = (ceil(cols / (64*VEC)), G); block = 4 waves sharing one 64*VEC-column tile; each wave
 // strides over rows with 4 rows in flight (ILP), and the 4 waves' column sums are combined
 // through LDS into one partial row per block row-group.
-template <typename T, int VEC, int ACT>
+template <typename T, int VEC, int ACT, int NT>
 __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ u,
                                                       T* __restrict__ du, float* __restrict__ part,
                                                       T* __restrict__ yout, int rows, int cols) {
   constexpr bool kAct = ACT != kNone;
+#define LD(p, o) do { if (NT & 1) vload_nt<T, VEC>(p, o); else vload<T, VEC>(p, o); } while (0)
+#define ST(p, o) do { if (NT & 2) vstore_nt<T, VEC>(p, o); else vstore<T, VEC>(p, o); } while (0)
   __shared__ float sh[4][64 * VEC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = (blockIdx.x * 64 + lane) * VEC;
@@ -118,8 +120,8 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, 
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const size_t off = (size_t)(r + k * stride) * cols + col;
-        vload<T, VEC>(dy + off, d[k]);
-        if (kAct) vload<T, VEC>(u + off, x[k]);
+        LD(dy + off, d[k]);
+        if (kAct) LD(u + off, x[k]);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -131,12 +133,12 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, 
             act_fdf<ACT>(x[k][j], a[j], g);
             d[k][j] *= g;
           }
-          vstore<T, VEC>(yout + (size_t)(r + k * stride) * cols + col, a);
+          ST(yout + (size_t)(r + k * stride) * cols + col, a);
         } else if (kAct) {
 #pragma unroll
           for (int j = 0; j < VEC; ++j) d[k][j] *= act_df<ACT>(x[k][j]);
         }
-        if (du) vstore<T, VEC>(du + (size_t)(r + k * stride) * cols + col, d[k]);
+        if (du) ST(du + (size_t)(r + k * stride) * cols + col, d[k]);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) acc[j] += d[k][j];
       }
@@ -144,10 +146,10 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, 
     for (; r < rows; r += stride) {
       const size_t off = (size_t)r * cols + col;
       float d[VEC];
-      vload<T, VEC>(dy + off, d);
+      LD(dy + off, d);
       if (kAct) {
         float x[VEC];
-        vload<T, VEC>(u + off, x);
+        LD(u + off, x);
         if (yout) {
           float a[VEC];
 #pragma unroll
@@ -156,17 +158,19 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, 
             act_fdf<ACT>(x[j], a[j], g);
             d[j] *= g;
           }
-          vstore<T, VEC>(yout + off, a);
+          ST(yout + off, a);
         } else {
 #pragma unroll
           for (int j = 0; j < VEC; ++j) d[j] *= act_df<ACT>(x[j]);
         }
       }
-      if (du) vstore<T, VEC>(du + off, d);
+      if (du) ST(du + off, d);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) acc[j] += d[j];
     }
   }
+#undef LD
+#undef ST
   if (!part) return;
 #pragma unroll
   for (int j = 0; j < VEC; ++j) sh[w][lane * VEC + j] = acc[j];
@@ -181,9 +185,15 @@ template <typename T, int VEC>
 void launch_act_bwd(const void* dy, const void* u, void* du, float* part, void* yout, int rows, int cols, int act,
                     int groups, hipStream_t s) {
   dim3 grid((cols / VEC + 63) / 64, groups);
-#define DTD_ACT_BWD(A)                                                                                          \
-  hipLaunchKernelGGL((act_bwd_kernel<T, VEC, A>), grid, dim3(256), 0, s, (const T*)dy, (const T*)u, (T*)du, part, \
+  const int nt = ew_nt_bits();
+#define DTD_ACT_BWD_NT(A, N)                                                                                    \
+  hipLaunchKernelGGL((act_bwd_kernel<T, VEC, A, N>), grid, dim3(256), 0, s, (const T*)dy, (const T*)u, (T*)du, part, \
                      (T*)yout, rows, cols)
+#define DTD_ACT_BWD(A)                                                                                          \
+  switch (nt) {                                                                                                 \
+    case 3: DTD_ACT_BWD_NT(A, 3); break;                                                                        \
+    default: DTD_ACT_BWD_NT(A, 0); break;                                                                       \
+  }
   switch (act) {
     case kGeluErf: DTD_ACT_BWD(kGeluErf); break;
     case kGeluTanh: DTD_ACT_BWD(kGeluTanh); break;
@@ -191,6 +201,7 @@ void launch_act_bwd(const void* dy, const void* u, void* du, float* part, void* 
     default: DTD_ACT_BWD(kNone); break;
   }
 #undef DTD_ACT_BWD
+#undef DTD_ACT_BWD_NT
 }
 
 template <typename T>
@@ -251,10 +262,16 @@ __global__ void __launch_bounds__(1024) colsum_finalize_kernel(FinalizeSet fs, i
 
 DTD_EXPORT int dtd_act_fwd(int dtype, const void* u, void* y, size_t n, int act, hipStream_t s) {
   if (n == 0) return 0;
+  const int mode = ew_mode(), nt = ew_nt_bits();
   size_t blocks = (n / 8 + 255) / 256;
   if (blocks < 1) blocks = 1;
-  if (blocks > 4096) blocks = 4096;
-#define DTD_ACT_FWD(T, A) hipLaunchKernelGGL((act_fwd_kernel<T, A>), dim3(blocks), dim3(256), 0, s, (const T*)u, (T*)y, n)
+  if (mode == 0 && blocks > 4096) blocks = 4096;   // streaming form: one 16-byte vector per thread
+#define DTD_ACT_FWD_NT(T, A, N) hipLaunchKernelGGL((act_fwd_kernel<T, A, N>), dim3(blocks), dim3(256), 0, s, (const T*)u, (T*)y, n)
+#define DTD_ACT_FWD(T, A)                         \
+  switch (nt) {                                   \
+    case 3: DTD_ACT_FWD_NT(T, A, 3); break;       \
+    default: DTD_ACT_FWD_NT(T, A, 0); break;      \
+  }
 #define DTD_ACT_FWD_T(T)                                \
   switch (act) {                                        \
     case kGeluErf: DTD_ACT_FWD(T, kGeluErf); break;     \
@@ -265,6 +282,7 @@ DTD_EXPORT int dtd_act_fwd(int dtype, const void* u, void* y, size_t n, int act,
   if (dtype == kBF16) { DTD_ACT_FWD_T(bf16) } else { DTD_ACT_FWD_T(float) }
 #undef DTD_ACT_FWD_T
 #undef DTD_ACT_FWD
+#undef DTD_ACT_FWD_NT
   DTD_LAUNCH_CHECK();
 }
 

@@ -122,6 +122,61 @@ template <int N> struct Vec<bf16, N> {
 template <typename T, int N> __device__ __forceinline__ void vload(const T* p, float* o) { Vec<T, N>::load(p, o); }
 template <typename T, int N> __device__ __forceinline__ void vstore(T* p, const float* i) { Vec<T, N>::store(p, i); }
 
+// Access form of the streaming elementwise kernels (GELU fwd/bwd, bias-grad, LayerNorm wave
+// kernels): non-temporal 16/8-byte loads AND stores of the [rows, h] tensors (NT = 3) and one
+// vector per thread -- +0.35 % whole-step, same box, two A/B sessions (profiles/r1_ab_ew_mode.jsonl;
+// NT loads only, NT stores only and plain one-vector-per-thread all measured lower).
+// DTD_EW_MODE=0 selects the plain grid-stride form (tuning runs).
+inline int ew_mode() {
+  const char* e = getenv("DTD_EW_MODE");
+  return e ? atoi(e) : 2;
+}
+inline int ew_nt_bits() { return ew_mode() == 2 ? 3 : 0; }
+
+// Streaming (non-temporal) forms for bf16 tensors touched once per pass: the 16-byte accesses
+// carry the nt hint, so a pass over a tensor larger than L2 + MALL does not evict what the
+// next kernel re-reads.  Other types / widths fall back to the plain forms.
+template <typename T, int N> __device__ __forceinline__ void vload_nt(const T* p, float* o) {
+  if constexpr (sizeof(T) == 2 && N % 8 == 0) {
+#pragma unroll
+    for (int i = 0; i < N; i += 8) {
+      const bf16x8 v = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p + i));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[i + j] = (float)v[j];
+    }
+  } else if constexpr (sizeof(T) == 2 && N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+      const bf16x4 v = __builtin_nontemporal_load(reinterpret_cast<const bf16x4*>(p + i));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[i + j] = (float)v[j];
+    }
+  } else {
+    vload<T, N>(p, o);
+  }
+}
+template <typename T, int N> __device__ __forceinline__ void vstore_nt(T* p, const float* in) {
+  if constexpr (sizeof(T) == 2 && N % 8 == 0) {
+#pragma unroll
+    for (int i = 0; i < N; i += 8) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)in[i + j];
+      __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p + i));
+    }
+  } else if constexpr (sizeof(T) == 2 && N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+      bf16x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (bf16)in[i + j];
+      __builtin_nontemporal_store(v, reinterpret_cast<bf16x4*>(p + i));
+    }
+  } else {
+    vstore<T, N>(p, in);
+  }
+}
+
 // ---- wave / block reductions (64-wide waves) ----
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -50,9 +50,13 @@ __device__ __forceinline__ float row_sum(float v) {
   return v;
 }
 
+// NT bit 0 / bit 1: streaming (non-temporal) loads / stores of the [rows, h] tensors (common.h)
+#define LDNT(p, o) do { if (NT & 1) vload_nt<T, VEC>(p, o); else vload<T, VEC>(p, o); } while (0)
+#define STNT(p, o) do { if (NT & 2) vstore_nt<T, VEC>(p, o); else vstore<T, VEC>(p, o); } while (0)
+
 // LPR lanes per row (64, or 32 = two rows per wave so that h = 768 / 1280 rows still move in
 // 16-byte bf16x8 vectors: 768 = 32 lanes x 3 x 8).
-template <typename T, int VEC, int ITERS, int LPR>
+template <typename T, int VEC, int ITERS, int LPR, int NT>
 __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
   constexpr int NPL = VEC * ITERS, RPW = 64 / LPR;
   const int lane = threadIdx.x & 63, sub = lane % LPR;
@@ -71,7 +75,7 @@ __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
     const int col = (c * LPR + sub) * VEC;
     float t[VEC];
     if (a.y) {
-      vload<T, VEC>((const T*)a.y + base + col, t);
+      LDNT((const T*)a.y + base + col, t);
       if (has_drop) {
 #pragma unroll
         for (int j = 0; j < VEC; ++j) t[j] *= drop_factor(g, base + col + j, thr, scale);
@@ -82,11 +86,11 @@ __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
     }
     if (a.r) {
       float rr[VEC];
-      vload<T, VEC>((const T*)a.r + base + col, rr);
+      LDNT((const T*)a.r + base + col, rr);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) t[j] += rr[j];
     }
-    if (a.z && valid) vstore<T, VEC>((T*)a.z + base + col, t);
+    if (a.z && valid) STNT((T*)a.z + base + col, t);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) z[c * VEC + j] = t[j];
   }
@@ -108,13 +112,13 @@ __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
     vload<T, VEC>((const T*)a.beta + col, bt);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) o[j] = (z[c * VEC + j] - mu) * rs * gm[j] + bt[j];
-    vstore<T, VEC>((T*)a.out + base + col, o);
+    STNT((T*)a.out + base + col, o);
   }
 }
 
 // One row per wave (the two-rows-per-wave layout of the forward doubles this kernel's per-lane
 // state and costs occupancy).
-template <typename T, int VEC, int ITERS>
+template <typename T, int VEC, int ITERS, int NT>
 __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
   constexpr int NPL = VEC * ITERS, LPR = 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6, sub = lane;
@@ -138,11 +142,11 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
     for (int c = 0; c < ITERS; ++c) {
       const int col = (c * LPR + sub) * VEC;
       float zz[VEC], dd[VEC];
-      vload<T, VEC>((const T*)a.z + base + col, zz);
-      vload<T, VEC>((const T*)a.dout + base + col, dd);
+      LDNT((const T*)a.z + base + col, zz);
+      LDNT((const T*)a.dout + base + col, dd);
       if (a.dout2) {
         float e[VEC];
-        vload<T, VEC>((const T*)a.dout2 + base + col, e);
+        LDNT((const T*)a.dout2 + base + col, e);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) dd[j] += e[j];
       }
@@ -169,11 +173,11 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
       }
       if (a.dz_extra) {
         float e[VEC];
-        vload<T, VEC>((const T*)a.dz_extra + base + col, e);
+        LDNT((const T*)a.dz_extra + base + col, e);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) dz[j] += e[j];
       }
-      if (a.dz) vstore<T, VEC>((T*)a.dz + base + col, dz);
+      if (a.dz) STNT((T*)a.dz + base + col, dz);
       if (a.dy) {
         float dy[VEC];
 #pragma unroll
@@ -181,7 +185,7 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
           dy[j] = has_drop ? dz[j] * drop_factor(g, base + col + j, thr, scale) : dz[j];
           py[c * VEC + j] += dy[j];
         }
-        vstore<T, VEC>((T*)a.dy + base + col, dy);
+        STNT((T*)a.dy + base + col, dy);
       }
     }
   }
@@ -205,6 +209,9 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
     }
   }
 }
+
+#undef LDNT
+#undef STNT
 
 // ---- generic block-per-row kernels (any even h; used for h > 2048) ----
 template <typename T>
@@ -325,12 +332,19 @@ template <typename T, int VEC, int ITERS, int LPR = 64>
 bool try_wave(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream_t s) {
   const int h = f ? f->h : b->h;
   if (h != LPR * VEC * ITERS) return false;
+  const int nt = ew_nt_bits();
   if (f) {
     const int rows_per_block = 4 * (64 / LPR);
-    hipLaunchKernelGGL((ln_fwd_wave<T, VEC, ITERS, LPR>), dim3((f->rows + rows_per_block - 1) / rows_per_block),
-                       dim3(256), 0, s, *f);
+    const dim3 grid((f->rows + rows_per_block - 1) / rows_per_block);
+    switch (nt) {
+      case 3: hipLaunchKernelGGL((ln_fwd_wave<T, VEC, ITERS, LPR, 3>), grid, dim3(256), 0, s, *f); break;
+      default: hipLaunchKernelGGL((ln_fwd_wave<T, VEC, ITERS, LPR, 0>), grid, dim3(256), 0, s, *f); break;
+    }
   } else {
-    hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS>), dim3(nblocks_bwd), dim3(256), 0, s, *b);
+    switch (nt) {
+      case 3: hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, 3>), dim3(nblocks_bwd), dim3(256), 0, s, *b); break;
+      default: hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, 0>), dim3(nblocks_bwd), dim3(256), 0, s, *b); break;
+    }
   }
   return true;
 }
