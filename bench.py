@@ -6,10 +6,11 @@ timed here is the full training step of the reference's ``data_parallel_training
 (forward with MLM labels -> backward with bucketed gradient all-reduce -> Adam step), on
 bert-base-cased geometry (108.3 M parameters, random init), seq 512, synthetic MLM batches
 with the reference masking law, bf16 compute with fp32 master weights.  Per-GPU batch is
-fixed as N grows (weak scaling); the default 128 x 512 tokens per GPU (the reference ran 4 on a
-16 GB T4) uses ~35 GB of the 288 GB HBM, runs the GEMMs at their large-M efficiency
-(1.0-1.4 PF/s) and amortises the per-step gradient all-reduce over a ~55 ms step.  Each rank
-draws its own dropout masks (seed offset by rank).
+fixed as N grows (weak scaling); the default 256 x 512 tokens per GPU (the reference ran 4 on a
+16 GB T4) uses ~70 GB of the 288 GB HBM, runs the GEMMs at their large-M efficiency
+(1.0-1.4 PF/s, TunableOp table measured at this shape) and amortises the per-step gradient
+all-reduce over a ~100 ms step (b256 vs b128: +2.1 % tokens/s same box; b384/b512 add < 1 %).
+Each rank draws its own dropout masks (seed offset by rank).
 
   python bench.py --gpus N --steps K --warmup W
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -39,7 +40,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="base")
-    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("DTD_BENCH_BATCH", "128")),
+    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("DTD_BENCH_BATCH", "256")),
                     help="per-GPU micro-batch (sequences)")
     ap.add_argument("--seq-len", type=int, default=512)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -201,6 +202,7 @@ def main():
                 "tuned_gemms": tuned,
                 "hip_graph": graphed is not None,
                 "async_wgrad": args.async_wgrad == "on",
+                "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if cuda else None,
             },
             "loss_first": round(first_loss, 4),
             "loss_last": round(float(loss.detach()), 4),

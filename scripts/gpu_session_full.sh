@@ -7,6 +7,6 @@ step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeo
 step bench_default 300 python bench.py
 step bench_default2 300 python bench.py
 if [ -n "$PROF" ]; then
-  step prof_b128 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_b128 -o run --output-format csv -- python bench.py --steps 5 --warmup 2
+  step prof_default 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_default -o run --output-format csv -- python bench.py --steps 5 --warmup 2
 fi
 echo done
