@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+from pathlib import Path
 import threading
 
 import torch  # noqa: F401  (must be imported first: binds libamdhip64 to torch's runtime)
@@ -86,7 +87,10 @@ def lib():
         if _LIB is not None:
             return _LIB
         path = _build.LIB_PATH
-        if os.environ.get("DTD_NO_BUILD") != "1" and _build.needs_build():
+        override = os.environ.get("DTD_KERNELS_SO")   # A/B runs: an alternative build of the library
+        if override:
+            path = Path(override)
+        elif os.environ.get("DTD_NO_BUILD") != "1" and _build.needs_build():
             _build.build(verbose=True)
         if not path.exists():
             raise KernelError(f"HIP kernel library missing: {path} (run ops/build.py)")

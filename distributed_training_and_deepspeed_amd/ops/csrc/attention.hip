@@ -100,6 +100,13 @@ __device__ __forceinline__ uint32_t half_word(uint32_t w, int hh) { return w >> 
 // used by the tests to check that deferral does not change the result beyond rounding).
 constexpr float kRescaleThr = 8.f;
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// Packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth of work per VALU
+// issue) for the per-score softmax / dropout math of the backward kernels, which is VALU-bound.
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 pk2(float x, float y) { return f32x2{x, y}; }
+__device__ __forceinline__ float mask_bits(float v, int m) { return __int_as_float(__float_as_int(v) & m); }
+
 __device__ __forceinline__ float keep_of(const DropoutRng& g, uint64_t e, uint32_t thr) {
   const uint32_t b = g.bits(e >> 1);
   const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
@@ -413,7 +420,9 @@ struct BwdArgs {
 
 // dK, dV: grid (ceil(S/128), B*H); block 256 = 4 waves x 32 keys ("key on the lane").
 // Query tiles of 64 rows (Q, dO row-major in LDS, double-buffered).
-template <int D, int OCC, int BM>
+// DROP / ALIBI are compile-time so that the hot path has no runtime branch (whose register
+// merges cost 16 v_mov per query sub-block) and no bias add without ALiBi.
+template <int D, int OCC, int BM, bool DROP, bool ALIBI>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   constexpr int QP = D + 8, NC = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * QP];
@@ -430,7 +439,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   const bool kvalid = key < S;
   const float sl2 = a.slopes ? a.slopes[h] * kLog2e : 0.f;
   const float sc2 = a.scale * kLog2e;
-  const bool drop = a.maskB != nullptr;
+  constexpr bool drop = DROP;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
   const float kbias = sl2 * (float)key;   // ALiBi bias of this lane's key (0 without ALiBi)
   const uint32_t* mcol = drop ? a.maskB + (size_t)bh * a.W * S + (kvalid ? key : 0) : nullptr;
@@ -459,8 +468,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   auto load_stats = [&](int q0) {
     if (threadIdx.x < BM) {
       const int qq = q0 + threadIdx.x;
-      lse_r = qq < S ? lseb[qq] * kLog2e : 0.f;
-      del_r = qq < S ? delb[qq] : 0.f;
+      lse_r = qq < S ? -lseb[qq] * kLog2e : 0.f;   // stored negated: P = 2^fma(s, sc2, -lse)
+      del_r = qq < S ? -delb[qq] : 0.f;            //                 dS = P (dP - delta)
     }
   };
   // dropout keep words of a query tile (one per 32 query rows), prefetched a tile ahead with
@@ -519,8 +528,16 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
         L4[g] = *reinterpret_cast<const f32x4*>(&lse_s[buf][qb * 32 + 8 * g + 4 * hh]);
         D4[g] = *reinterpret_cast<const f32x4*>(&del_s[buf][qb * 32 + 8 * g + 4 * hh]);
       }
+      // P = 2^(s sc2 + kbias - lse): score pairs (i, i+1) share a row group, so the row terms pair up
+      const f32x2 sc2v = pk2(sc2, sc2), kb2 = pk2(kbias, kbias);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[i] = fexp2(fmaf(sacc[i], sc2, kbias - L4[i >> 2][i & 3]));  // P
+      for (int i = 0; i < 16; i += 2) {
+        f32x2 nl = pk2(L4[i >> 2][i & 3], L4[i >> 2][(i & 3) + 1]);
+        if constexpr (ALIBI) nl += kb2;
+        const f32x2 x = pk_fma(pk2(sacc[i], sacc[i + 1]), sc2v, nl);
+        sacc[i] = fexp2(x.x);
+        sacc[i + 1] = fexp2(x.y);
+      }
       if (needmask) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -529,15 +546,23 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
           sacc[i] = ok ? sacc[i] : 0.f;
         }
       }
-      if (drop) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          pacc[i] = sacc[i] * fmaf(keep_bits(pacc[i], mw, crow(i, 0)), inv_keep, -D4[i >> 2][i & 3]);  // dS
-          sacc[i] = keep_bits(sacc[i], mw, crow(i, 0));                                          // P*mask (dV)
+      for (int i = 0; i < 16; i += 2) {
+        const f32x2 nd = pk2(D4[i >> 2][i & 3], D4[i >> 2][(i & 3) + 1]);
+        if constexpr (DROP) {
+          const int m0 = __builtin_amdgcn_sbfe((int)mw, crow(i, 0), 1);
+          const int m1 = __builtin_amdgcn_sbfe((int)mw, crow(i + 1, 0), 1);
+          const f32x2 t = pk_fma(pk2(mask_bits(pacc[i], m0), mask_bits(pacc[i + 1], m1)), pk2(inv_keep, inv_keep), nd);
+          const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * t;                 // dS
+          pacc[i] = ds.x;
+          pacc[i + 1] = ds.y;
+          sacc[i] = mask_bits(sacc[i], m0);                               // P*mask (dV)
+          sacc[i + 1] = mask_bits(sacc[i + 1], m1);
+        } else {
+          const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * (pk2(pacc[i], pacc[i + 1]) + nd);
+          pacc[i] = ds.x;
+          pacc[i + 1] = ds.y;
         }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) pacc[i] = sacc[i] * (pacc[i] - D4[i >> 2][i & 3]);
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -822,6 +847,15 @@ DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, con
   DTD_LAUNCH_CHECK();
 }
 
+template <int D, int OCC, int BM>
+static void launch_dkdv(dim3 grid, hipStream_t s, const BwdArgs& a) {
+  const bool drop = a.maskB != nullptr, alibi = a.slopes != nullptr;
+  if (drop && alibi) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, true, true>), grid, dim3(256), 0, s, a);
+  else if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, true, false>), grid, dim3(256), 0, s, a);
+  else if (alibi) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, false, true>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, false, false>), grid, dim3(256), 0, s, a);
+}
+
 // dq/dk/dv: bf16 views with row stride ld into dqkv.  `delta` is [B,H,S] fp32 scratch.
 DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                             const float* lse, float* delta, const uint32_t* masks, void* dq, void* dk, void* dv,
@@ -846,13 +880,13 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
     // query tile of the dK/dV loop: 128 rows halves the barriers / exposed load latency per
     // query row at 2 blocks per CU (75 KB LDS each); DTD_ATTN_DKDV_BM=64 selects the old tile
     const int bm = getenv("DTD_ATTN_DKDV_BM") ? atoi(getenv("DTD_ATTN_DKDV_BM")) : 128;
-    if (bm == 128 && occupancy(1) == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 1, 128>), grid, dim3(256), 0, s, a);
-    else if (bm == 128) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 128>), grid, dim3(256), 0, s, a);
-    else if (occupancy(1) >= 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, 1, 64>), grid, dim3(256), 0, s, a);
+    if (bm == 128 && occupancy(1) == 1) launch_dkdv<64, 1, 128>(grid, s, a);
+    else if (bm == 128) launch_dkdv<64, 2, 128>(grid, s, a);
+    else if (occupancy(1) >= 2) launch_dkdv<64, 2, 64>(grid, s, a);
+    else launch_dkdv<64, 1, 64>(grid, s, a);
   } else {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<128, 1, 64, 2>), grid, dim3(256), 0, s, a);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<128, 1, 64>), grid, dim3(256), 0, s, a);
+    launch_dkdv<128, 1, 64>(grid, s, a);
   }
   DTD_LAUNCH_CHECK();
 }
