@@ -47,6 +47,7 @@ def test_local_allreduce_average_and_many_epochs():
 
 
 def _ipc_rank(rank, world, port, out):
+    import time
     """Real (IPC) mode: `world` processes on the same GPU map each other's staging and signal buffers
     through hipIpcOpenMemHandle, exactly as ranks on different GPUs of a node do."""
     from distributed_training_and_deepspeed_amd import comm
@@ -63,6 +64,15 @@ def _ipc_rank(rank, world, port, out):
                 for x in xs[1:]:
                     ref += x.float()
                 mine = xs[rank].cuda()
+                # uneven arrival: ranks reach the barrier at different times (host sleep on odd
+                # ranks, a queued GEMM ahead of the kernel on rank 0) -- the spin barrier must
+                # wait, not time out or read stale peer data
+                if rank % 2:
+                    time.sleep(0.02)
+                if rank == 0:
+                    big = torch.randn(2048, 2048, device="cuda")
+                    for _ in range(8):
+                        big = big @ big * 1e-3
                 ar.all_reduce(mine, average=(it == 1))
                 torch.cuda.synchronize()
                 want = (ref / world if it == 1 else ref).to(dtype)
