@@ -1,0 +1,14 @@
+#!/usr/bin/env bash
+# GPU session: build, smoke, kernel/model tests, benches, rocprof stats.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+source scripts/gpu_step.sh
+step build 300 python -c "import __graft_entry__ as g; g.build()"
+step pytest_gpu 900 python -m pytest tests -m gpu -q
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench_b4 300 python bench.py --steps 10 --warmup 3 --batch-size 4
+step bench_b32 300 python bench.py --steps 10 --warmup 3 --batch-size 32
+step bench_ref_b4 300 python bench.py --steps 10 --warmup 3 --batch-size 4 --impl reference
+step bench_ref_b32 300 python bench.py --steps 10 --warmup 3 --batch-size 32 --impl reference
+export TMPDIR=/tmp
+step rocprof_b32 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_b32 -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --batch-size 32
+echo done

@@ -1,0 +1,16 @@
+#!/usr/bin/env bash
+# Perf session: tests, benches at b32/b64, TunableOp tuning pass, rocprof of the best config.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+source scripts/gpu_step.sh
+step build 300 python -c "import __graft_entry__ as g; g.build()"
+step pytest_gpu 900 python -m pytest tests -m gpu -q -x
+step bench_b32 300 python bench.py --steps 10 --warmup 3 --batch-size 32
+step bench_b64 300 python bench.py --steps 10 --warmup 3 --batch-size 64
+step bench_b4 300 python bench.py --steps 10 --warmup 3 --batch-size 4
+export TMPDIR=/tmp
+step rocprof_b32 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_b32 -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --batch-size 32
+export PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_FILENAME=gpurun_out/tunableop_results%d.csv
+step bench_b32_tune 900 python bench.py --steps 4 --warmup 2 --batch-size 32
+export PYTORCH_TUNABLEOP_TUNING=0
+step bench_b32_tuned 300 python bench.py --steps 10 --warmup 3 --batch-size 32
+echo done
