@@ -7,7 +7,7 @@ timed here is the full training step of the reference's ``data_parallel_training
 bert-base-cased geometry (108.3 M parameters, random init), seq 512, synthetic MLM batches
 with the reference masking law, bf16 compute with fp32 master weights.  Per-GPU batch is
 fixed as N grows (weak scaling); the default 256 x 512 tokens per GPU (the reference ran 4 on a
-16 GB T4) uses ~70 GB of the 288 GB HBM, runs the GEMMs at their large-M efficiency
+16 GB T4) peaks at ~47 GB of the 288 GB HBM, runs the GEMMs at their large-M efficiency
 (1.0-1.4 PF/s, TunableOp table measured at this shape) and amortises the per-step gradient
 all-reduce over a ~100 ms step (b256 vs b128: +2.1 % tokens/s same box; b384/b512 add < 1 %).
 Each rank draws its own dropout masks (seed offset by rank).

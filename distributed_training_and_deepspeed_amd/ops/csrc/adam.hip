@@ -41,6 +41,14 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   }
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// One 8-element group per thread (no grid-stride loop) with non-temporal 16-byte loads and
+// stores: every byte is touched exactly once, so keeping it out of L2/MALL only costs reuse
+// that does not exist, and a flat grid keeps more bytes in flight per CU than a 2048-block
+// grid-stride loop (the same change moved the streaming GELU / LayerNorm kernels from ~4.9 to
+// ~6 TB/s, profiles/r1_elementwise_roofline.jsonl).
+template <bool GBF16>
 __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
   const float lr = a.hp[0], b1 = a.hp[1], b2 = a.hp[2], eps = a.hp[3], wd = a.hp[4];
   const float step = a.hp[5], gs = a.hp[6];
@@ -49,32 +57,50 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
     bc1 = 1.f - powf(b1, step);
     bc2s = sqrtf(1.f - powf(b2, step));
   }
-  const size_t nv = a.n / 4;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x) {
-    float4 p = reinterpret_cast<float4*>(a.p)[i];
-    float4 m = reinterpret_cast<float4*>(a.m)[i];
-    float4 v = reinterpret_cast<float4*>(a.v)[i];
-    float g[4];
-    if (a.g_dtype == kBF16) vload<bf16, 4>((const bf16*)a.g + i * 4, g);
-    else vload<float, 4>((const float*)a.g + i * 4, g);
-    adam_elem(p.x, m.x, v.x, g[0] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
-    adam_elem(p.y, m.y, v.y, g[1] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
-    adam_elem(p.z, m.z, v.z, g[2] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
-    adam_elem(p.w, m.w, v.w, g[3] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
-    reinterpret_cast<float4*>(a.p)[i] = p;
-    reinterpret_cast<float4*>(a.m)[i] = m;
-    reinterpret_cast<float4*>(a.v)[i] = v;
-    if (a.p_lp) {
-      const float q[4] = {p.x, p.y, p.z, p.w};
-      vstore<bf16, 4>(a.p_lp + i * 4, q);
+  const size_t ng = a.n / 8;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i < ng) {
+    f32x4* P = reinterpret_cast<f32x4*>(a.p) + 2 * i;
+    f32x4* M = reinterpret_cast<f32x4*>(a.m) + 2 * i;
+    f32x4* V = reinterpret_cast<f32x4*>(a.v) + 2 * i;
+    f32x4 p0 = __builtin_nontemporal_load(P), p1 = __builtin_nontemporal_load(P + 1);
+    f32x4 m0 = __builtin_nontemporal_load(M), m1 = __builtin_nontemporal_load(M + 1);
+    f32x4 v0 = __builtin_nontemporal_load(V), v1 = __builtin_nontemporal_load(V + 1);
+    float g[8];
+    if constexpr (GBF16) {
+      vload_nt<bf16, 8>((const bf16*)a.g + i * 8, g);
+    } else {
+      const f32x4* G = reinterpret_cast<const f32x4*>(a.g) + 2 * i;
+      const f32x4 g0 = __builtin_nontemporal_load(G), g1 = __builtin_nontemporal_load(G + 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { g[j] = g0[j]; g[4 + j] = g1[j]; }
     }
+    float q[8], mm[8], vv[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      q[j] = p0[j]; q[4 + j] = p1[j];
+      mm[j] = m0[j]; mm[4 + j] = m1[j];
+      vv[j] = v0[j]; vv[4 + j] = v1[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adam_elem(q[j], mm[j], vv[j], g[j] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p0[j] = q[j]; p1[j] = q[4 + j];
+      m0[j] = mm[j]; m1[j] = mm[4 + j];
+      v0[j] = vv[j]; v1[j] = vv[4 + j];
+    }
+    __builtin_nontemporal_store(p0, P); __builtin_nontemporal_store(p1, P + 1);
+    __builtin_nontemporal_store(m0, M); __builtin_nontemporal_store(m1, M + 1);
+    __builtin_nontemporal_store(v0, V); __builtin_nontemporal_store(v1, V + 1);
+    if (a.p_lp) vstore_nt<bf16, 8>(a.p_lp + i * 8, q);
   }
-  if (blockIdx.x == 0) {
-    for (size_t e = nv * 4 + threadIdx.x; e < a.n; e += blockDim.x) {
-      float g = a.g_dtype == kBF16 ? (float)((const bf16*)a.g)[e] : ((const float*)a.g)[e];
-      adam_elem(a.p[e], a.m[e], a.v[e], g * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
-      if (a.p_lp) a.p_lp[e] = (bf16)a.p[e];
-    }
+  // tail (n % 8 elements): the first threads of the last block
+  const size_t e = ng * 8 + threadIdx.x;
+  if (blockIdx.x == gridDim.x - 1 && e < a.n) {
+    float g = GBF16 ? (float)((const bf16*)a.g)[e] : ((const float*)a.g)[e];
+    adam_elem(a.p[e], a.m[e], a.v[e], g * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
+    if (a.p_lp) a.p_lp[e] = (bf16)a.p[e];
   }
 }
 
@@ -125,7 +151,10 @@ DTD_EXPORT int dtd_adam_step(float* p, float* m, float* v, const void* g, int g_
                              const float* hp, int mode, hipStream_t s) {
   if (n == 0) return 0;
   AdamArgs a{p, m, v, g, (bf16*)p_lp, n, hp, mode, g_dtype};
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, a);
+  // 8 elements per thread; at least one block so the tail always has an owner
+  const size_t blocks = (n / 8 + 255) / 256 > 0 ? (n / 8 + 255) / 256 : 1;
+  if (g_dtype == kBF16) hipLaunchKernelGGL(adam_kernel<true>, dim3(blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(adam_kernel<false>, dim3(blocks), dim3(256), 0, s, a);
   DTD_LAUNCH_CHECK();
 }
 
