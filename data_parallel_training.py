@@ -77,21 +77,22 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
             model.rt.rng.advance()
         return out.loss.detach()
 
-    graphed = None
+    graphed, batches, warm, loss = None, iter(loader), [], None
     if opts.graph and cuda:
         # whole step (forward, backward + bucket all-reduces, optimizer, RNG advance) replayed as
         # one hipGraph: the reference's 4 x 512-token batches are host-launch bound otherwise
         from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep, mlm_capacity
         model.rt.mlm_capacity = mlm_capacity(batch_size * opts.seq_len)
-        ex = dataset[0:batch_size]
-        graphed = CapturedStep(step, {"input_ids": ex["input_ids"].to(device), "labels": ex["labels"].to(device)},
-                               runtime=model.rt)
+        warm = [b for _, b in zip(range(min(3, training_steps)), batches)]
+        graphed = None if not warm else CapturedStep(step, warm[0], warmup_batches=warm, runtime=model.rt)
+        loss = graphed.warmup_losses[-1] if graphed is not None else None
+        if progress is not None:
+            progress.update(len(warm))
 
     timer = StepTimer(batch_size * opts.seq_len, world_size)
     start = time.time()
-    n = 0
-    loss = None
-    for batch in loader:
+    n = 0  # timed steps (graph warm-up steps trained before the clock started)
+    for batch in batches:
         timer.start()
         if graphed is not None and batch["input_ids"].shape == graphed.static["input_ids"].shape:
             loss = graphed(input_ids=batch["input_ids"], labels=batch["labels"])
@@ -107,11 +108,11 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
     if graphed is not None:
         graphed.check()
     if opts.save_dir:
-        save_checkpoint(os.path.join(opts.save_dir, "ddp_checkpoint.pt"), model, optimizer, step=n)
+        save_checkpoint(os.path.join(opts.save_dir, "ddp_checkpoint.pt"), model, optimizer, step=n + len(warm))
     print(f"\nTotal Training Time: {elapsed:.2f} seconds")
     if rank == 0:
         tokens = n * batch_size * opts.seq_len * world_size
-        print(json.dumps({"tokens_per_s": round(tokens / max(elapsed, 1e-9), 1), "steps_per_rank": n,
+        print(json.dumps({"tokens_per_s": round(tokens / max(elapsed, 1e-9), 1), "steps_per_rank": n + len(warm), "timed_steps": n,
                           "world_size": world_size, "final_loss": round(float(loss.detach()), 4) if loss is not None else None}))
         if opts.metrics_json:
             timer.write(opts.metrics_json, {"model": name, "per_gpu_batch": batch_size, "seq_len": opts.seq_len,

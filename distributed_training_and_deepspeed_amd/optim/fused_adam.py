@@ -182,7 +182,9 @@ class FusedAdam(torch.optim.Optimizer):
             p.grad = None
 
     def state_dict(self):
-        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+        # under hipGraph replay only the device copy of the step count advances
+        step = int(self.hp[5].item()) if self.hp.is_cuda else self.step_count
+        return {"step": step, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
                 "master": self.master, "param_groups": [{k: v for k, v in g.items() if k != "params"}
                                                          for g in self.param_groups]}
 

@@ -30,25 +30,31 @@ def mlm_capacity(tokens: int, p: float = 0.15, sigmas: float = 8.0) -> int:
 
 
 class CapturedStep:
-    def __init__(self, step_fn, static_inputs: dict, warmup: int = 3, runtime=None):
+    def __init__(self, step_fn, static_inputs: dict, warmup: int = 3, runtime=None, warmup_batches=None):
         """``step_fn(**inputs)`` runs one full training step and returns a tensor (the loss).
         ``warmup`` real steps run eagerly on a side stream first (library handles, GEMM
-        solution lookup and allocator pools must exist before capture)."""
+        solution lookup and allocator pools must exist before capture).  ``warmup_batches``
+        (list of input dicts): run those batches as the warm-up steps instead of repeating
+        ``static_inputs``, so a trainer can count them as its first training steps (the
+        capture itself computes nothing: only replays do); their losses are in
+        ``self.warmup_losses``."""
         self.rt = runtime
         if runtime is not None and runtime.mlm_overflow is None:
             runtime.mlm_overflow = torch.zeros((), dtype=torch.bool, device="cuda")
         self.static = {k: v.detach().clone() for k, v in static_inputs.items()}
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        batches = list(warmup_batches) if warmup_batches is not None else [self.static] * warmup
+        self.warmup_losses = []
         with torch.cuda.stream(side):
-            for _ in range(warmup):
-                step_fn(**self.static)
+            for b in batches:
+                self.warmup_losses.append(step_fn(**b))
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = step_fn(**self.static)
-        self.warmup = warmup
+        self.warmup = len(batches)
 
     def __call__(self, **inputs):
         for k, v in inputs.items():

@@ -79,26 +79,27 @@ def train(model_name, batch_size, training_steps, stage, opts):
         model_engine.step()
         return outputs.loss.detach()
 
-    graphed = None
+    graphed, batches, warm = None, iter(loader), []
     if graph:
         # whole step (forward, backward + gradient reduction, fused Adam, parameter refresh,
         # dropout-RNG advance) replayed as one hipGraph: batch 1 x 512 is host-launch bound.
         # Captured before the clock starts (3 eager warm-up steps on the first batch, like
         # data_parallel_training.py --graph)
         from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep
-        ex = dataset[0:batch_size]
-        graphed = CapturedStep(train_step, {"input_ids": ex["input_ids"].to(device), "labels": ex["labels"].to(device)},
-                               runtime=getattr(model, "rt", None))
+        warm = [b for _, b in zip(range(min(3, training_steps)), batches)]
+        graphed = None if not warm else CapturedStep(train_step, warm[0], warmup_batches=warm, runtime=getattr(model, "rt", None))
+        loss = graphed.warmup_losses[-1] if graphed is not None else None
     start = time.time()
     progress = None
     if rank == 0 and not opts.quiet:
         try:
             from tqdm import tqdm
             progress = tqdm(range(training_steps))
+            progress.update(len(warm))
         except ImportError:
             pass
-    n = 0
-    for batch in loader:
+    n = 0  # timed steps (graph warm-up steps trained before the clock started)
+    for batch in batches:
         if graphed is not None and batch["input_ids"].shape == graphed.static["input_ids"].shape:
             loss = graphed(input_ids=batch["input_ids"], labels=batch["labels"])
         else:
