@@ -78,7 +78,9 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
         return out.loss.detach()
 
     graphed, batches, warm, loss = None, iter(loader), [], None
-    if opts.graph and cuda:
+    if opts.graph == "auto":  # multi-rank RCCL capture stays opt-in
+        opts.graph = "on" if (cuda and world_size == 1 and batch_size <= 32 and not opts.markers) else "off"
+    if opts.graph == "on" and cuda:
         # whole step (forward, backward + bucket all-reduces, optimizer, RNG advance) replayed as
         # one hipGraph: the reference's 4 x 512-token batches are host-launch bound otherwise
         from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep, mlm_capacity
@@ -137,8 +139,9 @@ if __name__ == "__main__":
     parser.add_argument("--markers", action="store_true", help="roctx ranges per phase (rocprofv3 --marker-trace)")
     parser.add_argument("--save-dir", default="", help="write <dir>/ddp_checkpoint.pt at the end")
     parser.add_argument("--resume", default="", help="checkpoint file to resume from")
-    parser.add_argument("--graph", action="store_true",
-                        help="capture the whole training step in a hipGraph and replay it (small batches)")
+    parser.add_argument("--graph", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                        help="capture the whole training step in a hipGraph and replay it (auto: on for one GPU "
+                             "at <= 32 sequences per step, where the step is host-launch bound)")
     args = parser.parse_args()
 
     device_count = args.device_count or get_device_count()

@@ -84,3 +84,24 @@ def test_captured_zero_step_matches_eager(stage):
         assert torch.equal(ea.master, eb.master)
     finally:
         comm.destroy()
+
+
+def test_zero_script_graph_trains_like_eager():
+    """zero_dp_training.py end to end: --graph (default on one GPU) warms up on the first real
+    batches and replays the rest -- the same steps on the same batches as --graph off."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for mode in ("off", "on"):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(32000 + os.getpid() % 1000 + len(res)))
+        out = subprocess.run([sys.executable, os.path.join(root, "zero_dp_training.py"), "--model-name", "causal-tiny",
+                              "--training-steps", "8", "--seq-len", "128", "--batch-size", "2", "--quiet",
+                              "--no-memstats", "--graph", mode],
+                             env=env, capture_output=True, text=True, timeout=100, cwd=root)
+        assert out.returncode == 0, out.stderr[-2000:]
+        res[mode] = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["on"]["hip_graph"] and not res["off"]["hip_graph"]
+    assert res["on"]["final_loss"] == res["off"]["final_loss"]

@@ -48,7 +48,9 @@ def train(model_name, batch_size, training_steps, stage, opts):
     cfg = get_config(model_name)
     model = build_model(model_name, dtype=dtype, device=device, seed=0, impl=opts.impl)
 
-    graph = opts.graph and cuda
+    if opts.graph == "auto":  # multi-rank RCCL capture stays opt-in
+        opts.graph = "on" if (cuda and world_size == 1 and stage <= 1) else "off"
+    graph = opts.graph == "on" and cuda
     if graph and stage > 1:
         raise SystemExit("--graph supports ZeRO stages 0 and 1 (stage 2/3 allocate gradient landing / "
                          "gathered-parameter buffers per step)")
@@ -144,8 +146,9 @@ if __name__ == "__main__":
     parser.add_argument("--impl", default="auto", choices=["auto", "fused", "reference"])
     parser.add_argument("--num-gpus", type=int, default=None, help="spawn locally (like `deepspeed --num_gpus`)")
     parser.add_argument("--no-memstats", action="store_true")
-    parser.add_argument("--graph", action="store_true",
-                        help="stages 0/1: capture the whole training step in a hipGraph and replay it (small batches)")
+    parser.add_argument("--graph", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                        help="stages 0/1: capture the whole training step in a hipGraph and replay it "
+                             "(auto: on for one GPU at stage 0/1, where batch-1 steps are host-launch bound)")
     parser.add_argument("--quiet", action="store_true")
     args, extra_args = parser.parse_known_args()
     if args.num_gpus and "WORLD_SIZE" not in os.environ:
