@@ -94,9 +94,26 @@ class IdleTimeTracker:
             self._add(idx, max(0.0, a.elapsed_time(b)))
         self._pending = []
 
+    def _collect_ready(self) -> None:
+        """Resolve the event pairs that have already completed, without blocking: a per-step
+        synchronize would stop the host from queueing the next step while the GPU runs this
+        one (2-stage BERT-base b16 on one GPU: 36 ms host-serialised vs 14 ms of kernels)."""
+        still = []
+        for idx, a, b in self._pending:
+            if b.query():
+                self._add(idx, max(0.0, a.elapsed_time(b)))
+            else:
+                still.append((idx, a, b))
+        self._pending = still
+        if len(self._pending) > 4096:   # bound the number of live events
+            self.collect()
+
     def step_boundary(self) -> None:
         """Idle time is accumulated within a training step (not across optimizer steps)."""
-        self.collect()
+        if self.timing == "host":
+            self.collect()
+        else:
+            self._collect_ready()
         self._last = {}
 
     def table(self, steps: int) -> list[list]:
