@@ -54,7 +54,10 @@ def main():
     parser.add_argument("--seq-len", type=int, default=512)
     parser.add_argument("--devices", default=None, help="explicit stage devices, e.g. cuda:0,cuda:1")
     parser.add_argument("--timing", default="device", choices=["device", "host"])
-    parser.add_argument("--checkpoint", default="except_last", choices=["except_last", "always", "never"])
+    parser.add_argument("--checkpoint", default="auto", choices=["auto", "except_last", "always", "never"],
+                        help="GPipe activation recompute. auto: 'never' when every stage device has >= 64 GB "
+                             "(MI355X: 288 GB holds all micro-batches' activations; recompute cost +50%% step "
+                             "time, profiles/r1_gpipe_recompute.jsonl), else torch Pipe's 'except_last'")
     parser.add_argument("--impl", default="auto", choices=["auto", "fused", "reference"])
     parser.add_argument("--schedule", default="gpipe", choices=["gpipe", "1f1b"],
                         help="pipeline schedule: torch-Pipe fill-drain (reference) or 1F1B (S live micro-batches)")
@@ -65,6 +68,10 @@ def main():
     devices = args.devices.split(",") if args.devices else None
     bert = BertModelWithMP(config=config, device_count=args.device_count, verbose=args.verbose, devices=devices,
                            dtype=dtype, impl=args.impl, timing=args.timing)
+    if args.checkpoint == "auto":
+        big = all(d.type == "cuda" and torch.cuda.get_device_properties(d).total_memory >= 64 * 2 ** 30
+                  for d in bert.group_devices)
+        args.checkpoint = "never" if big else "except_last"
     model = bert.to_pipeline(chunks=args.micro_batch_count, checkpoint=args.checkpoint) if args.pipeline else bert
 
     optimizer = PerDeviceOptimizer(model.parameters(), torch_adamw, lr=5e-5)
@@ -111,6 +118,7 @@ def main():
     rows = summarize_idle_time(bert, args.training_steps)
     print(json.dumps({"tokens_per_s": round(n * args.batch_size * args.seq_len / max(elapsed, 1e-9), 1),
                       "pipeline": args.pipeline, "stages": len(bert.group_devices),
+                      "checkpoint": args.checkpoint if args.pipeline else None,
                       "idle_ms_per_step": [round(r[1], 3) for r in rows[1:]],
                       "final_loss": round(float(loss.detach()), 4) if loss is not None else None}))
 
