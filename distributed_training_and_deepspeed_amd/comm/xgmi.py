@@ -11,7 +11,10 @@ caller's stream that reads the peers' buffers directly over the xGMI full mesh:
 * ``two-shot`` (larger, ``numel % (8 world) == 0``): reduce-scatter + all-gather through the
   peers' result buffers -- 2(n-1)/n of the bytes per GPU, all 7 links busy at once.
 
-Results are bitwise identical on every rank (fixed summation order).  Messages above
+Results are bitwise identical on every rank (fixed summation order).  Every barrier spin is
+bounded: when a peer never arrives the kernel sets a device error flag and still finishes, so
+that call's result is summed over possibly stale peer data (CORRUPT) -- callers must poll
+``error()`` (DDP does every ``xgmi_check_every`` steps and raises).  Messages above
 ``max_bytes`` or with odd sizes fall back to RCCL.  ``XgmiAllReduce.local(world)`` builds the
 single-process variant (``world`` virtual ranks on one GPU) used by the tests on a 1-GPU box.
 

@@ -98,13 +98,32 @@ class DeviceBatchLoader:
         return out
 
     def __iter__(self):
-        nxt = None
-        for ix in self._batches():
-            cur = self._load(ix) if nxt is None else nxt
-            if self._stream is not None:
-                torch.cuda.current_stream(self.device).wait_stream(self._stream)
-                for t in cur.values():
-                    t.record_stream(torch.cuda.current_stream(self.device))
-            nxt = None
-            yield cur
-        return
+        # one batch ahead: batch i+1's gather + H2D copy is issued on the side stream before
+        # batch i is handed out, so it overlaps batch i's compute; the compute stream waits
+        # only on the event recorded after the copy of the batch it is about to consume
+        it = self._batches()
+        ix = next(it, None)
+        if ix is None:
+            return
+        cur, ev = self._load(ix), self._record()
+        for ix in it:
+            nxt = self._load(ix)
+            nev = self._record()
+            yield self._handoff(cur, ev)
+            cur, ev = nxt, nev
+        yield self._handoff(cur, ev)
+
+    def _record(self):
+        if self._stream is None:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(self._stream)
+        return ev
+
+    def _handoff(self, batch, ev):
+        if ev is not None:
+            cs = torch.cuda.current_stream(self.device)
+            cs.wait_event(ev)
+            for t in batch.values():
+                t.record_stream(cs)   # the side-stream allocation is not recycled under compute
+        return batch

@@ -66,7 +66,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, bucket_cap_mb: float = 25.0,
                  grad_dtype: torch.dtype | None = None, process_group=None, broadcast_parameters: bool = True,
                  overlap: bool = True, flatten_params: bool = True, small_bucket_allreduce: str = "rccl",
-                 xgmi_max_mb: float = 4.0, async_wgrad: bool = False):
+                 xgmi_max_mb: float = 4.0, async_wgrad: bool = False, xgmi_check_every: int = 100):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -86,6 +86,11 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
         self._xgmi = None
+        # a timed-out xGMI barrier (a peer never arrived) leaves the bucket holding a sum over
+        # stale peer data; the kernel only raises a device flag, so finish() reads it every
+        # ``xgmi_check_every`` synced steps (one host sync) and raises
+        self._xgmi_check_every = max(1, int(xgmi_check_every))
+        self._xgmi_steps = 0
         if small_bucket_allreduce == "xgmi" and self.world > 1 and self.backend == "nccl":
             from ..comm.xgmi import XgmiAllReduce
             self._xgmi = XgmiAllReduce(process_group, max_bytes=int(xgmi_max_mb * 2 ** 20))
@@ -194,6 +199,9 @@ class DistributedDataParallel(nn.Module):
             b.work = comm_log.all_reduce(view, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
 
     def _finish_backward(self) -> None:
+        # one end-of-backward callback per backward pass, synced or not: the next backward
+        # (e.g. the synced micro-step after a no_sync one) must queue its own
+        self._callback_queued = False
         if not self._sync_enabled:
             return
         self.finish()
@@ -215,6 +223,17 @@ class DistributedDataParallel(nn.Module):
                 b.work = None
         self.grads.expose_as_grad()
         self._need_reset = True
+        if self._xgmi is not None:
+            self._xgmi_steps += 1
+            if self._xgmi_steps % self._xgmi_check_every == 0:
+                self.check_xgmi()
+
+    def check_xgmi(self) -> None:
+        """Raise if any native xGMI all-reduce barrier timed out since creation (its results
+        were computed from peer buffers that may be stale: the gradients are corrupt)."""
+        if self._xgmi is not None and self._xgmi.error():
+            raise RuntimeError("xGMI all-reduce barrier timed out (a peer rank never arrived): "
+                               "the small-bucket gradients of this run are corrupt")
 
     # ------------------------------------------------------------------ conveniences
     def zero_grad(self, set_to_none: bool = True) -> None:

@@ -612,6 +612,11 @@ class ZeroEngine(nn.Module):
     @torch.no_grad()
     def save_checkpoint(self, save_dir: str, tag=None, client_state: dict | None = None,
                         save_latest: bool = True) -> str:
+        # under hipGraph replay (zero_dp_training.py --graph) the host counters stop advancing
+        # after capture; the optimizer's device step count (hp[5]) is the truth for both the
+        # Adam bias correction and the engine's global step
+        opt_step = int(self.optimizer.state_dict()["step"])
+        self.global_steps = max(self.global_steps, opt_step)
         tag = str(tag) if tag is not None else f"global_step{self.global_steps}"
         path = os.path.join(save_dir, tag)
         if self.rank == 0:
@@ -622,7 +627,7 @@ class ZeroEngine(nn.Module):
         opt = self.optimizer
         if self.stage > 0 or self.rank == 0:      # stage 0: the state is replicated
             torch.save({"master": self.master.detach().cpu(), "exp_avg": opt.exp_avg.detach().cpu(),
-                        "exp_avg_sq": opt.exp_avg_sq.detach().cpu(), "step": opt.step_count,
+                        "exp_avg_sq": opt.exp_avg_sq.detach().cpu(), "step": opt_step,
                         "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in opt.param_groups],
                         "stage": self.stage, "world": self.world, "shard_numel": self.shard_numel,
                         "global_steps": self.global_steps}, self._shard_file(path))
@@ -663,8 +668,8 @@ class ZeroEngine(nn.Module):
             self._load_full(ms["module"])
         self.global_steps = int(ms.get("global_steps", 0))
         rt = getattr(self.module, "rt", None)
-        if rt is not None and ms.get("dropout_rng") is not None:   # dropout masks continue the same stream
-            rt.rng.state.copy_(ms["dropout_rng"])
+        if rt is not None and ms.get("dropout_rng") is not None:   # dropout masks continue at the saved step;
+            rt.rng.state[1:2].copy_(ms["dropout_rng"][1:2])         # each rank keeps its own seed
         self._need_reset = True
         self._ckpt_barrier()
         return path, ms.get("client_state", {})

@@ -4,7 +4,10 @@ SURVEY.md 5.4: the reference saves nothing (weights come from ``from_pretrained`
 framework adds save/resume.  ZeRO engines have their own sharded layout
 (``parallel/zero.py::ZeroEngine.save_checkpoint``).  Here every rank holds the same state, so
 rank 0 writes one file with the module state, the optimizer state (fp32 master + moments for
-``FusedAdam``), the step and the device-resident dropout RNG state, and every rank loads it.
+``FusedAdam``), the step and the step of the device-resident dropout RNG, and every rank loads
+it.  The dropout SEED is per rank (trainers reseed by rank so replicas draw independent masks)
+and is not in the file: a resumed rank keeps the seed it was started with and continues the
+saved step, exactly as if the run had not been interrupted.
 Loading uses ``torch.load(weights_only=True)`` only.
 """
 from __future__ import annotations
@@ -37,7 +40,9 @@ def save_checkpoint(path: str, model: torch.nn.Module, optimizer=None, step: int
         state = {"module": _cpu(model.state_dict()), "step": int(step), "extra": extra or {},
                  "optimizer": _cpu(optimizer.state_dict()) if optimizer is not None and hasattr(optimizer, "state_dict")
                  else None,
-                 "dropout_rng": rt.rng.state.detach().cpu() if rt is not None else None}
+                 # only the step of the dropout stream: every rank keeps its own seed (DDP
+                 # trainers reseed per rank so replicas draw independent masks)
+                 "dropout_step": int(rt.rng.state[1].item()) if rt is not None else None}
         tmp = path + ".tmp"
         torch.save(state, tmp)
         os.replace(tmp, path)                  # never leave a half-written checkpoint behind
@@ -54,6 +59,6 @@ def load_checkpoint(path: str, model: torch.nn.Module, optimizer=None) -> dict:
     if optimizer is not None and state.get("optimizer") is not None:
         optimizer.load_state_dict(state["optimizer"])
     rt = getattr(model, "rt", None)
-    if rt is not None and state.get("dropout_rng") is not None:
-        rt.rng.state.copy_(state["dropout_rng"])
+    if rt is not None and state.get("dropout_step") is not None:
+        rt.rng.state[1:2].fill_(int(state["dropout_step"]))   # this rank's seed stays as it is
     return {"step": state["step"], "extra": state["extra"]}

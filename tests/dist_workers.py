@@ -42,6 +42,27 @@ def ddp_worker(rank, world, port, out_dir, model_name, impl, n_steps, bucket_mb)
     comm.destroy()
 
 
+def ddp_nosync_worker(rank, world, port, out_dir, impl):
+    """Gradient accumulation through DDP.no_sync(): micro-batch 0 without communication, micro-
+    batch 1 synced (accumulated average), then a fresh synced step on micro-batch 2 (must not
+    accumulate and must still all-reduce)."""
+    from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
+    comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
+    model = build_model("tiny", impl=impl, seed=3)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=0.05)
+    ids, lab = _batches(model.cfg, rank, world, 3)
+    with ddp.no_sync():
+        ddp(ids[0], labels=lab[0]).loss.backward()
+    ddp(ids[1], labels=lab[1]).loss.backward()
+    acc = {n: p.main_grad.detach().clone() for n, p in model.named_parameters()}
+    ddp.zero_grad()
+    ddp(ids[2], labels=lab[2]).loss.backward()
+    fresh = {n: p.main_grad.detach().clone() for n, p in model.named_parameters()}
+    if rank == 0:
+        torch.save({"acc": acc, "fresh": fresh}, os.path.join(out_dir, "nosync.pt"))
+    comm.destroy()
+
+
 def zero_worker(rank, world, port, out_dir, model_name, stage, n_steps, gas):
     from distributed_training_and_deepspeed_amd.comm import logger as clog
     from distributed_training_and_deepspeed_amd.parallel.zero import initialize
@@ -108,7 +129,8 @@ def zero_ckpt_worker(rank, world, port, out_dir, stage, load_stage):
     run(a, range(2, 4))
     fa = a.full_state_dict()
     b = engine(load_stage, 99)
-    path, client = b.load_checkpoint(ck)
+    b.module.rt.rng.reseed(a.module.rt.rng.seed)   # restarted rank: same dropout seed as before,
+    path, client = b.load_checkpoint(ck)           # the checkpoint restores only the step
     gs = b.global_steps
     loaded = b.full_state_dict()
     run(b, range(2, 4))

@@ -36,3 +36,31 @@ def test_load_wikitext_mlm_and_causal(tmp_path):
     assert torch.equal(c.labels, c.input_ids) and (c.labels == 0).any()   # causal: pads included (quirk 8)
     sub = ds.select(range(10))
     assert sub.input_ids.shape == (10, 32)
+
+
+def test_device_batch_loader_prefetch_order_and_contents():
+    """The one-ahead prefetching loader yields every sampler batch, in order, with the rows the
+    sampler named (incl. the short last batch) -- CPU path; the side-stream path is exercised
+    by the GPU trainers."""
+    import torch
+
+    from distributed_training_and_deepspeed_amd.data import DeviceBatchLoader, DistributedSampler
+
+    class DS:
+        def __init__(self, n):
+            self.input_ids = torch.arange(n * 4).view(n, 4)
+            self.labels = -self.input_ids
+
+        def __len__(self):
+            return self.input_ids.shape[0]
+
+    ds = DS(11)
+    sampler = DistributedSampler(ds, num_replicas=1, rank=0, shuffle=True, seed=5)
+    order = list(iter(sampler))
+    loader = DeviceBatchLoader(ds, batch_size=4, sampler=sampler)
+    got = list(loader)
+    assert len(got) == len(loader) == 3
+    for i, b in enumerate(got):
+        ix = torch.as_tensor(order[4 * i:4 * i + 4])
+        assert torch.equal(b["input_ids"], ds.input_ids[ix]) and torch.equal(b["labels"], ds.labels[ix])
+    assert list(DeviceBatchLoader(DS(0), batch_size=4)) == []

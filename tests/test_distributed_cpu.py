@@ -43,6 +43,34 @@ def test_ddp_gradients_match_single_process(tmp_path, free_port, impl):
         assert err <= 1e-5 * (g.abs().max().item() + 1e-6), (n, err)
 
 
+@pytest.mark.parametrize("impl", ["fused", "reference"])
+def test_ddp_no_sync_accumulation(tmp_path, free_port, impl):
+    """no_sync micro-step + synced micro-step == sum of both micro-batches' averaged gradients;
+    the following step starts a fresh window and is all-reduced (a no_sync backward
+    used to leave the end-of-backward callback flag set, so later steps never synchronised)."""
+    world = 2
+    _spawn(W.ddp_nosync_worker, world, free_port, str(tmp_path), impl)
+    res = torch.load(tmp_path / "nosync.pt", weights_only=True)
+    model = build_model("tiny", impl=impl, seed=3)
+
+    def avg_grads(mbs):
+        g = {n: torch.zeros_like(p) for n, p in model.named_parameters()}
+        for r in range(world):
+            ids, lab = W._batches(model.cfg, r, world, 3)
+            for i in mbs:
+                model.zero_grad(set_to_none=True)
+                model(ids[i], labels=lab[i]).loss.backward()
+                for n, p in model.named_parameters():
+                    g[n] += p.grad / world
+        return g
+
+    for key, mbs in (("acc", (0, 1)), ("fresh", (2,))):
+        ref = avg_grads(mbs)
+        for n, g in ref.items():
+            err = (res[key][n] - g).abs().max().item()
+            assert err <= 1e-5 * (g.abs().max().item() + 1e-6), (key, n, err)
+
+
 def _full_params(res, world):
     """Rebuild {segment index: full flat} from the per-rank master shards."""
     out = []

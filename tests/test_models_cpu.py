@@ -155,8 +155,14 @@ def test_replicated_checkpoint_resume_is_exact(tmp_path):
     save_checkpoint(str(tmp_path / "ck.pt"), a, oa, step=2, extra={"note": "x"})
     for i in range(2, 4):
         step(a, oa, i)
+    # the resumed process is started like the original (same per-rank dropout seed); the file
+    # restores the parameters, the optimizer and the dropout STEP but never overrides the seed
     b = build_model("tiny", seed=11)
+    b.rt.rng.reseed(a.rt.rng.seed)
     ob = hf_adamw(b.parameters(), lr=1e-3)
+    c = build_model("tiny", seed=11)                 # another rank: its own seed survives the load
+    meta = load_checkpoint(str(tmp_path / "ck.pt"), c, hf_adamw(c.parameters(), lr=1e-3))
+    assert int(c.rt.rng.state[0]) == 11 and int(c.rt.rng.state[1]) == 2
     meta = load_checkpoint(str(tmp_path / "ck.pt"), b, ob)
     assert meta == {"step": 2, "extra": {"note": "x"}}
     for i in range(2, 4):
