@@ -25,6 +25,7 @@ from torch import nn
 
 from ..ops import attention as A
 from ..ops import functional as Fx
+from ..ops import gemm as G
 from ..ops.grad import emit_wgrad, grad_done, grad_dst, note_use
 from ..ops.rng import RngState, attn_keep_mask
 from .config import TransformerConfig
@@ -200,6 +201,13 @@ def _acc(p):
     return grad_dst(p)
 
 
+def _ffn_gemm_ok(c, x: torch.Tensor, w: torch.Tensor, *more) -> bool:
+    """The hand-written GEMM with the GELU epilogues (ops/csrc/gemm.hip) takes the FFN products
+    when the activation is GELU(erf), the tensors are bf16 on the GPU and the shape tiles by 256."""
+    return (c.activation == "gelu" and x.is_cuda and x.dtype == torch.bfloat16 and G.enabled()
+            and G.supported(x.shape[0], w.shape[0], x.shape[1], x, w, *more))
+
+
 class _FusedLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, layer: TransformerLayer, *params):
@@ -234,8 +242,11 @@ class _FusedLayerFn(torch.autograd.Function):
             z1, f_in, m2, r2 = Fx.ln_fwd(o, x2d, g2, b2, eps, p_h, rng, s1)
         else:
             z1, f_in, m1, r1 = Fx.ln_fwd(o, x2d, g1, b1, eps, p_h, rng, s1)
-        u = F.linear(f_in, w1, bf1)
-        a = Fx.act_fwd(u, c.activation)
+        if G.ffn_fwd_enabled() and _ffn_gemm_ok(c, f_in, w1):
+            u, a = G.linear_gelu(f_in, w1, bf1)     # fc1 + bias + GELU in one kernel
+        else:
+            u = F.linear(f_in, w1, bf1)
+            a = Fx.act_fwd(u, c.activation)
         y = F.linear(a, w2, bf2)
         if c.pre_ln:
             out = Fx.dropout_add(y, z1, p_h, rng, s2)
@@ -276,11 +287,20 @@ class _FusedLayerFn(torch.autograd.Function):
                 grad_done(p)
         # dgrad first; without a kept forward activation, a = act(u) (fc2's wgrad input) is
         # recomputed inside the activation-backward pass (no separate act_fwd read/write)
-        da = dy @ w2
-        if a is None:
-            du, a = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1), want_act=True)
+        w2t = None
+        if (a is not None and G.ffn_bwd_enabled() and c.activation == "gelu" and dy.is_cuda
+                and dy.dtype == torch.bfloat16 and G.supported(dy.shape[0], w2.shape[1], dy.shape[1], dy, u)):
+            w2t = G.transpose(w2)                      # [ffn, hidden]: K-contiguous B operand
+        if w2t is not None:
+            # fc2 dgrad, GELU' and fc1's bias gradient in one kernel (no da round trip)
+            du = G.gelu_bwd_gemm(dy, w2t, u, dbias=_acc(bf1))
+            del w2t
         else:
-            du = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1))
+            da = dy @ w2
+            if a is None:
+                du, a = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1), want_act=True)
+            else:
+                du = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1))
         grad_done(bf1)
         emit_wgrad(w2, dy, a, async_ok=True)
         del a

@@ -1,54 +1,96 @@
-// MFMA GEMM with fused epilogues for the transformer FFN (gfx950).
+// MFMA GEMM with fused transformer epilogues for gfx950 (MI355X / CDNA4).
 //
 //   C[M, N] = A[M, K] . B[N, K]^T        bf16 in, fp32 accumulate, both operands K-contiguous
 //
-// hipBLASLt runs the plain projections; this kernel exists for the products whose OUTPUT feeds an
-// elementwise pass that would otherwise re-read it from HBM:
-//   EPI_STORE      C (+ bias[n])                         plain / bias GEMM (tests, reference point)
-//   EPI_BIAS_GELU  U = C + bias; A = gelu(U); store U, A    FFN up-projection forward (fc1 + GELU):
-//                                                         the activation pass's U re-read disappears
-//   EPI_GELU_BWD   dU = C * gelu'(U[m, n]); store dU;     FFN backward (fc2 dgrad + GELU'): the
-//                  column partial sums of dU (fc1 bias)   da round trip through HBM disappears
+// A Linear layer's forward is exactly this product (B = the [out, in] weight); its input-gradient
+// product uses B = W^T (a cached transposed copy, `dtd_transpose_bf16` below).  The epilogues fuse
+// the elementwise passes that would otherwise re-read the GEMM output from HBM:
+//   EPI_STORE      C = acc (+ bias[n])                          Linear forward / dgrad
+//   EPI_BIAS_GELU  U = acc + bias; A = gelu(U); store U and A    FFN up-projection forward
+//   EPI_GELU_BWD   dU = bf16(acc) * gelu'(U); store dU; column   FFN down-projection dgrad + GELU'
+//                  partial sums of dU (the up-projection's bias gradient, finalised by colsum)
+//   EPI_ADD        C = C + acc (in place)                       residual-branch dgrad (post-LN BERT)
 //
-// Structure (cdna_hip_programming.md §5): 256x256 output tile per 512-thread workgroup, 8 waves as
-// 2 (M) x 4 (N), each wave 128 x 64; K-steps of 64 staged global -> LDS with 16-byte LDS-DMA
-// (global_load_lds_dwordx4, no VGPR staging) into two LDS stages (2 x 64 KiB in ONE __shared__
-// array); the next K-step's DMA is in flight while the current one is multiplied, ordered by a
-// counted `s_waitcnt vmcnt` and raw s_barrier (no vmcnt(0) drain).  LDS rows are 128 B with the
-// 16-byte chunk index XOR-swizzled by (row & 7): DMA destinations stay lane-linear (the SOURCE
-// address carries the inverse swizzle, an involution) and every ds_read_b128 fragment read is
-// bank-conflict free.  MFMA v_mfma_f32_16x16x32_bf16 computes the transposed tile (B fragment as
-// the A operand), so each lane's accumulator holds 4 CONSECUTIVE columns of one row: epilogue
-// loads/stores are 8-byte bf16x4 row segments.  XCD-aware bijective tile order.
+// Main loop (cdna_hip_programming.md §5, "256² 8-phase template"): 256x256 output tile per
+// 512-thread workgroup, 8 waves as 2 (M) x 4 (N), each wave 128 x 64 as 8 x 4 tiles of
+// v_mfma_f32_16x16x32_bf16.  K-steps of 64 live in two 64 KiB LDS buffers (ONE __shared__ array);
+// each K-step is four phases, one per 64x32 quadrant of the wave's output (16 MFMAs each), and
+// every phase stages one quarter ("half-tile", 16 KiB) of the NEXT K-step by 16-byte LDS-DMA
+// (global_load_lds_dwordx4): A-rows-lo, B-cols-lo, B-cols-hi, A-rows-hi -- the order the next
+// K-step's phases read them.  A counted `s_waitcnt vmcnt(4)` per phase retires the DMA issued two
+// phases earlier (never vmcnt(0) in the loop), and raw s_barriers order it for the readers.
+// The two wave rows run one barrier apart (stagger): while one half of a SIMD's waves issues its
+// MFMAs the other half reads its LDS fragments, so the matrix pipe sees back-to-back MFMA
+// segments.  LDS rows are 128 B with the 16-byte chunk index XOR-swizzled by (row & 7): DMA
+// destinations stay lane-linear, the SOURCE address carries the (involutive) swizzle, and every
+// ds_read_b128 fragment read is bank-conflict free.  MFMAs take the B fragment as their first
+// operand (the tile is computed transposed), so a lane's accumulator holds 4 consecutive columns
+// of one row.
+//
+// Epilogue: the accumulators (with bias / residual added in fp32, one rounding) go to LDS as a
+// 256 x 256 bf16 image (8-byte column slots XOR-swizzled by row & 15: conflict-free writes), and
+// are read back row-major so every global store (and the GELU-backward U load) is a full 512-byte
+// row segment of 16-byte vectors.  XCD-aware bijective tile order (T1).
 #include "common.h"
 
 using namespace dtd;
 
 namespace {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
-constexpr int BM = 256, BK = 64;
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int A_BYTES = BM * BK * 2;             // 32 KiB
+constexpr int TILE_BYTES = (BM + BN) * BK * 2;   // 64 KiB per K-step buffer
+constexpr int LDS_BYTES = 2 * TILE_BYTES;        // 128 KiB
 
-enum Epi : int { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_GELU_BWD = 2 };
+enum Epi : int { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_GELU_BWD = 2, EPI_ADD = 3 };
 
 struct GemmArgs {
   const bf16* a; const bf16* b;          // A [M, K] (lda), B [N, K] (ldb)
-  bf16* c; int ldc;                      // output (STORE: C, BIAS_GELU: U, GELU_BWD: dU)
+  bf16* c;                               // STORE / ADD: C; BIAS_GELU: U; GELU_BWD: dU   (ldc)
   bf16* c2;                              // BIAS_GELU: A = gelu(U) (ldc)
-  const bf16* u; int ldu;                // GELU_BWD: pre-activation U
-  const bf16* bias;                      // [N] or null
-  float* part;                           // GELU_BWD: [M/128][N] column partials of dU (or null)
-  int M, N, K, lda, ldb;
+  const bf16* u;                         // GELU_BWD: pre-activation U (ldu)
+  const bf16* bias;                      // [N] or null (STORE, BIAS_GELU)
+  float* part;                           // GELU_BWD: [M / 256][N] fp32 column partials (or null)
+  int M, N, K, lda, ldb, ldc, ldu;
+  unsigned long long* stamps;            // diagnostic builds only (-DDTD_GEMM_STAMPS), else null
 };
+
+// In-kernel timing stamps (diagnostic build, scripts/gemm_stamps.py): lane 0 of wave 0 records
+// s_memtime at fixed points of each tile, plus the CU / XCC ids, with plain vector stores.
+#ifdef DTD_GEMM_STAMPS
+#define STAMP(slot, iter)                                                                          \
+  do {                                                                                             \
+    if (g.stamps && tid == 0 && (iter) < 32)                                                       \
+      g.stamps[((size_t)blockIdx.x * 32 + (iter)) * 8 + (slot)] = __builtin_amdgcn_s_memtime();    \
+  } while (0)
+#define STAMP_ID(iter)                                                                             \
+  do {                                                                                             \
+    if (g.stamps && tid == 0 && (iter) < 32)                                                       \
+      g.stamps[((size_t)blockIdx.x * 32 + (iter)) * 8 + 7] =                                       \
+          ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |                 \
+          __builtin_amdgcn_s_getreg((31 << 11) | 4);                                               \
+  } while (0)
+#else
+#define STAMP(slot, iter) do {} while (0)
+#define STAMP_ID(iter) do {} while (0)
+#endif
+
+// raw workgroup barrier (no vmcnt drain: LDS-DMA may stay in flight across it) that the compiler
+// also treats as a memory barrier, so no LDS access is hoisted or sunk across it
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// GELU(erf) and its derivative from one exponential (same formulas as act.hip)
+// GELU(erf) and its derivative from one exponential (the formulas of act.hip)
 __device__ __forceinline__ float phi_cdf(float x, float e) {
   const float a = fabsf(x) * 0.70710678118654752f;
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
@@ -62,218 +104,663 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return fmaf(x * 0.3989422804014327f, e, phi_cdf(x, e));
 }
 
-// bijective XCD remap of the linear workgroup id (dispatch deals ids round-robin over 8 XCDs)
+// bijective XCD remap of the linear workgroup id (dispatch deals ids round-robin over 8 XCDs):
+// each XCD gets a contiguous range of tiles, so tiles sharing an A panel share an L2
 __device__ __forceinline__ int xcd_remap(int id, int n) {
   const int q = n / 8, r = n % 8, x = id % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
 }
 
-// BN = 256: 8 waves as 2 (M) x 4 (N), 2 LDS stages of 64 KiB (one K-step in flight).
-// BN = 128: 8 waves as 4 (M) x 2 (N), 3 LDS stages of 48 KiB (two K-steps in flight).
-template <int EPI, int BN, int STAGES>
-__global__ void __launch_bounds__(512, 1) gemm_bt_kernel(GemmArgs g) {
-  constexpr int STAGE_BYTES = (BM + BN) * BK * 2;   // A rows then B rows, 128 B each
-  constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
-  constexpr int WM = BM / WAVES_M;                  // rows per wave (128 or 64)
-  constexpr int MI = WM / 16;                       // 16-row MFMA sub-tiles per wave
-  constexpr int A_DMA = BM / 64, B_DMA = BN / 64;   // 1 KiB DMA instructions per wave per K-step
-  constexpr int DMA = A_DMA + B_DMA;
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
+// buffer resource for a wave-uniform base pointer (readfirstlane makes the uniformity provable,
+// so hipcc emits plain buffer ops instead of waterfall loops: cdna_hip_programming.md T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// Per-lane byte offsets of this wave's 8 LDS-DMA rows within a tile's A / B panel (fixed for the
+// whole kernel): DMA i of half-tile H fills 8 rows starting at r0, lane L -> row r0 + L/8, chunk
+// slot L%8 <- global chunk (L%8) ^ (L/8)  (r0 is a multiple of 8, so (row & 7) == L/8).
+// H = 0: A rows {0-63, 128-191}, 1: B rows {64j + 0..31}, 2: B rows {64j + 32..63},
+// 3: A rows {64-127, 192-255}.
+struct StageOffs {
+  int a[2][2], b[2][2];   // [lo/hi half][dma]
+  int la[2][2], lb[2][2]; // LDS byte offsets of the 8-row groups
+};
+
+__device__ __forceinline__ StageOffs stage_offsets(int w, int lane, int lda, int ldb) {
+  StageOffs o;
+  const int dr = lane >> 3;
+  const int sc = ((lane & 7) ^ dr) * 8;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = w * 2 + i;   // 8-row group 0..15 of the half-tile
+      const int ra = (j >> 3) * 128 + (h ? 64 : 0) + 8 * (j & 7);
+      const int rb = (j >> 2) * 64 + (h ? 32 : 0) + 8 * (j & 3);
+      o.a[h][i] = ((ra + dr) * lda + sc) * 2;
+      o.b[h][i] = ((rb + dr) * ldb + sc) * 2;
+      o.la[h][i] = ra * 128;
+      o.lb[h][i] = A_BYTES + rb * 128;
+    }
+  return o;
+}
+
+// One half-tile (16 KiB = 128 rows x 128 B) of K-step kt into LDS buffer `buf` by
+// buffer_load_dwordx4 ... lds (32-bit lane offsets, the K-step as the scalar offset)
+template <int H>
+__device__ __forceinline__ void stage(const StageOffs& o, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb,
+                                      char* buf, int kt) {
+  const int so = kt * BK * 2;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if constexpr (H == 0 || H == 3) {
+      constexpr int h = H == 3 ? 1 : 0;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(buf + o.la[h][i]), 16, o.a[h][i], so, 0, 0);
+    } else {
+      constexpr int h = H == 2 ? 1 : 0;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(buf + o.lb[h][i]), 16, o.b[h][i], so, 0, 0);
+    }
+  }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 2) gemm_bt_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int li = lane & 15, lq = lane >> 4;
-  const int wm = w / WAVES_N, wn = w % WAVES_N;
+  const int li = lane & 15, lq = lane >> 4, sw = li & 7;
+  const int wm = w >> 2, wn = w & 3;
   const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn;
   const int t = xcd_remap(blockIdx.x, ntiles);
-  // M-major within an XCD's range: consecutive tiles share the B panel (the weight, L2 resident)
-  const int bm = t / ntn, bn = t % ntn;
+  const int bm = t / ntn, bn = t % ntn;   // N-minor: consecutive tiles share the A panel
   const int m0 = bm * BM, n0 = bn * BN;
   const int nk = g.K / BK;
 
-  // LDS-DMA of one K-step into stage s: each wave moves BM/8 rows of A and BN/8 rows of B, 8 rows
-  // (1 KiB) per instruction; lane L fills row row0 + L/8, chunk slot L%8 <- global chunk
-  // (L%8) ^ (row & 7).
-  const int drow = lane >> 3, dpos = lane & 7;
-  auto issue = [&](int kt, int s) {
-    char* base = smem + s * STAGE_BYTES;
-    const int k0 = kt * BK;
+  f32x4 acc[8][4];
 #pragma unroll
-    for (int i = 0; i < A_DMA; ++i) {
-      const int row0 = (w * A_DMA + i) * 8, r = row0 + drow;
-      const bf16* src = g.a + (size_t)(m0 + r) * g.lda + k0 + ((dpos ^ (r & 7)) * 8);
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(base + row0 * 128), 16, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < B_DMA; ++i) {
-      const int row0 = (w * B_DMA + i) * 8, r = row0 + drow;
-      const bf16* src = g.b + (size_t)(n0 + r) * g.ldb + k0 + ((dpos ^ (r & 7)) * 8);
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(base + BM * 128 + row0 * 128), 16, 0, 0);
-    }
-  };
-
-  f32x4 acc[MI][4];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  STAMP_ID(0);
+  STAMP(0, 0);
 
-  // STAGES-1 K-steps in flight: prologue issues them, each iteration issues kt+STAGES-1 and
-  // waits (counted) for kt's DMAs only
-#pragma unroll
-  for (int p = 0; p < STAGES - 1; ++p)
-    if (p < nk) issue(p, p);
+  // prologue: K-step 0 complete in buffer 0
+  const StageOffs so = stage_offsets(w, lane, g.lda, g.ldb);
+  const auto rsa = uniform_rsrc(g.a + (size_t)m0 * g.lda), rsb = uniform_rsrc(g.b + (size_t)n0 * g.ldb);
+  stage<0>(so, rsa, rsb, smem, 0);
+  stage<1>(so, rsa, rsb, smem, 0);
+  stage<2>(so, rsa, rsb, smem, 0);
+  stage<3>(so, rsa, rsb, smem, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  STAMP(1, 0);
+  if (__builtin_amdgcn_readfirstlane(wm) == 1) bar();   // stagger wave row 1
+
+  // fragment byte offsets within a buffer (row r, chunk c) -> r*128 + ((c ^ (r&7)) * 16)
+  const int arow = (wm * 128 + li) * 128;            // + mi*16 rows
+  const int brow = A_BYTES + (wn * 64 + li) * 128;   // + ni*16 rows
+  const int ch0 = ((0 * 4 + lq) ^ sw) * 16, ch1 = ((1 * 4 + lq) ^ sw) * 16;
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+
   for (int kt = 0; kt < nk; ++kt) {
-    const int s = kt % STAGES;
-    const int ahead = nk - 1 - kt < STAGES - 1 ? nk - 1 - kt : STAGES - 1;   // K-steps issued beyond kt
-    if (kt + STAGES - 1 < nk) {
-      issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
-      if constexpr (STAGES == 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(DMA) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * DMA) : "memory");
-    } else if (ahead >= 1 && STAGES == 3) {
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(DMA) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    const char* As = smem + s * STAGE_BYTES;
-    const char* Bs = As + BM * 128;
+    const char* cur = smem + (kt & 1) * TILE_BYTES;
+    char* nxt = smem + ((kt & 1) ^ 1) * TILE_BYTES;
+    const bool more = kt + 1 < nk;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int chunk = ks * 4 + lq;
-      bf16x8 af[MI], bfr[4];
+    for (int p = 0; p < 4; ++p) {
+      // ---- this phase's LDS fragments (quadrant order (0,0) (0,1) (1,1) (1,0))
+      if (p == 0 || p == 2) {
+        const int qm = p == 0 ? 0 : 1;
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int row = wn * 64 + ni * 16 + li;
-        bfr[ni] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((chunk ^ (row & 7)) * 16));
+        for (int mi = 0; mi < 4; ++mi) {
+          const char* r = cur + arow + (qm * 4 + mi) * 16 * 128;
+          af[mi][0] = *reinterpret_cast<const bf16x8*>(r + ch0);
+          af[mi][1] = *reinterpret_cast<const bf16x8*>(r + ch1);
+        }
       }
+      if (p == 0 || p == 1) {
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int row = wm * WM + mi * 16 + li;
-        af[mi] = *reinterpret_cast<const bf16x8*>(As + row * 128 + ((chunk ^ (row & 7)) * 16));
+        for (int ni = 0; ni < 2; ++ni) {
+          const char* r = cur + brow + (p * 2 + ni) * 16 * 128;
+          bf16x8 x0 = *reinterpret_cast<const bf16x8*>(r + ch0);
+          bf16x8 x1 = *reinterpret_cast<const bf16x8*>(r + ch1);
+          if (p == 0) { b0[ni][0] = x0; b0[ni][1] = x1; } else { b1[ni][0] = x0; b1[ni][1] = x1; }
+        }
       }
+      // ---- stage quarter p of the next K-step; retire the DMA of two phases ago
+      if (more) {
+        if (p == 0) stage<0>(so, rsa, rsb, nxt, kt + 1);
+        if (p == 1) stage<1>(so, rsa, rsb, nxt, kt + 1);
+        if (p == 2) stage<2>(so, rsa, rsb, nxt, kt + 1);
+        if (p == 3) stage<3>(so, rsa, rsb, nxt, kt + 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else if (p == 0) {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      bar();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      const int qm = (p == 2 || p == 3) ? 1 : 0;
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
+      for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(bfr[ni], af[mi], acc[mi][ni]);
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            const bf16x8 bb = (p == 1 || p == 2) ? b1[ni][ks] : b0[ni][ks];
+            const int nn = ((p == 1 || p == 2) ? 2 : 0) + ni;
+            acc[qm * 4 + mi][nn] = mfma16(bb, af[mi][ks], acc[qm * 4 + mi][nn]);
+          }
+      __builtin_amdgcn_s_setprio(0);
+      bar();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // stage s fully read before it is refilled
   }
+  if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
+  __syncthreads();
+  STAMP(2, 0);
 
-  // ---- epilogue: lane holds rows m = m0 + wm*WM + mi*16 + li, columns n = n0 + wn*64 + ni*16 + 4*lq + r
-  float colsum[4][4];
-  if constexpr (EPI == EPI_GELU_BWD) {
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) colsum[ni][r] = 0.f;
-  }
+  // ---- epilogue 1 (accumulator layout): lane holds C[m][n .. n+3], m = wm*128 + mi*16 + li,
+  //      n = wn*64 + ni*16 + 4*lq (tile-local).  fp32 bias / residual, one bf16 rounding, -> LDS.
+  char* img = smem;   // [256][512 B] bf16, 8-byte slot s of row r at slot s ^ (r & 15)
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) {
-    const int n = n0 + wn * 64 + ni * 16 + 4 * lq;
+    const int n = wn * 64 + ni * 16 + 4 * lq;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (EPI != EPI_GELU_BWD && g.bias) {
-      const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n);
+    if constexpr (EPI == EPI_STORE || EPI == EPI_BIAS_GELU) {
+      if (g.bias) {
+        const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n0 + n);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[r] = (float)b4[r];
+        for (int r = 0; r < 4; ++r) bv[r] = (float)b4[r];
+      }
     }
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-      const int m = m0 + wm * WM + mi * 16 + li;
-      const size_t off = (size_t)m * g.ldc + n;
-      bf16x4 o;
-      if constexpr (EPI == EPI_STORE) {
+    for (int mi = 0; mi < 8; ++mi) {
+      const int m = wm * 128 + mi * 16 + li;
+      float v[4];
+      if constexpr (EPI == EPI_ADD) {
+        const bf16x4 c4 = *reinterpret_cast<const bf16x4*>(g.c + (size_t)(m0 + m) * g.ldc + n0 + n);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[mi][ni][r] + bv[r]);
-        *reinterpret_cast<bf16x4*>(g.c + off) = o;
-      } else if constexpr (EPI == EPI_BIAS_GELU) {
-        bf16x4 o2;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bf16 uq = (bf16)(acc[mi][ni][r] + bv[r]);   // GELU of the STORED (bf16) U, as the
-          o[r] = uq;                                        // unfused path computes it
-          o2[r] = (bf16)gelu((float)uq);
-        }
-        *reinterpret_cast<bf16x4*>(g.c + off) = o;
-        *reinterpret_cast<bf16x4*>(g.c2 + off) = o2;
+        for (int r = 0; r < 4; ++r) v[r] = acc[mi][ni][r] + (float)c4[r];
       } else {
-        const bf16x4 u4 = *reinterpret_cast<const bf16x4*>(g.u + (size_t)m * g.ldu + n);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          // dA rounded to bf16 first: bit-compatible with the unfused (GEMM -> act_bwd) path
-          const float da = (float)(bf16)acc[mi][ni][r];
-          const float du = da * gelu_grad((float)u4[r]);
-          o[r] = (bf16)du;
-          colsum[ni][r] += du;
-        }
-        *reinterpret_cast<bf16x4*>(g.c + off) = o;
+        for (int r = 0; r < 4; ++r) v[r] = acc[mi][ni][r] + bv[r];
       }
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)v[r];
+      *reinterpret_cast<bf16x4*>(img + m * 512 + (((n >> 2) ^ (m & 15)) << 3)) = o;
     }
   }
+  __syncthreads();
+  STAMP(3, 0);
+
+  // ---- epilogue 2 (row layout): wave w stores rows w*32 .. w*32+31, two rows per instruction,
+  //      lane -> row r = w*32 + 2i + (lane >> 5), 16-byte chunk c = lane & 31 (8 columns)
+  const int c = lane & 31;
+  float colsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int r = w * 32 + 2 * i + (lane >> 5);
+    const int x = r & 15;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(img + r * 512 + ((c ^ (x >> 1)) << 4));
+    if (x & 1) v = __builtin_shufflevector(v, v, 4, 5, 6, 7, 0, 1, 2, 3);   // halves stored swapped
+    const size_t off = (size_t)(m0 + r) * g.ldc + n0 + c * 8;
+    if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
+      *reinterpret_cast<bf16x8*>(g.c + off) = v;
+    } else if constexpr (EPI == EPI_BIAS_GELU) {
+      bf16x8 a;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = (bf16)gelu((float)v[j]);   // GELU of the stored (bf16) U
+      *reinterpret_cast<bf16x8*>(g.c + off) = v;
+      *reinterpret_cast<bf16x8*>(g.c2 + off) = a;
+    } else {   // EPI_GELU_BWD: v = bf16(dA)
+      const bf16x8 u8 = *reinterpret_cast<const bf16x8*>(g.u + (size_t)(m0 + r) * g.ldu + n0 + c * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float du = (float)v[j] * gelu_grad((float)u8[j]);
+        o[j] = (bf16)du;
+        colsum[j] += du;
+      }
+      *reinterpret_cast<bf16x8*>(g.c + off) = o;
+    }
+  }
+  STAMP(4, 0);
+#ifdef DTD_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STAMP(5, 0);
+#endif
   if constexpr (EPI == EPI_GELU_BWD) {
     if (!g.part) return;
-    // sum over the 16 lanes sharing lq (16 rows each already summed over mi): xor 1,2,4,8
+    // lanes c and c+32 hold the same columns; then the 8 waves combine through LDS
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
+    for (int j = 0; j < 8; ++j) colsum[j] += __shfl_xor(colsum[j], 32, 64);
+    __syncthreads();   // the image is fully consumed
+    float* red = reinterpret_cast<float*>(smem);   // [8 waves][256 columns]
+    if (lane < 32) {
+      *reinterpret_cast<f32x4*>(red + w * 256 + c * 8) = f32x4{colsum[0], colsum[1], colsum[2], colsum[3]};
+      *reinterpret_cast<f32x4*>(red + w * 256 + c * 8 + 4) = f32x4{colsum[4], colsum[5], colsum[6], colsum[7]};
+    }
+    __syncthreads();
+    if (tid < 256) {
+      float s = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = colsum[ni][r];
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 4, 64);
-        v += __shfl_xor(v, 8, 64);
-        colsum[ni][r] = v;
+      for (int k = 0; k < 8; ++k) s += red[k * 256 + tid];
+      g.part[(size_t)bm * g.N + n0 + tid] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent form: one 512-thread workgroup per CU walks its tiles (XCD group x = blockIdx % 8
+// owns a contiguous tile range, its 32 workgroups take every 32nd tile of it, so the tiles in
+// flight on one XCD share A panels).  The K-step stream never drains between tiles: the last
+// K-step of a tile stages K-step 0 of the workgroup's NEXT tile into the other LDS buffer, so the
+// epilogue (two rounds through the free buffer, the stores as full row segments) runs while that
+// DMA lands, and there is no prologue or workgroup dispatch between tiles.  The first two phases
+// of a tile wait with vmcnt(4 + S) (S = the epilogue's vector-memory count): the DMA they retire
+// is older than the epilogue's stores, which may stay in flight.  (An epilogue storing straight
+// from the accumulators, 8-byte pieces, measured slower: scripts/gemm_stamps.py.)
+// vector-memory instructions every wave issues in one epilogue (loads + stores): the lower
+// bound of what sits between a K-step-0 DMA and the next tile's first waits
+constexpr int kStores(int epi) {
+  return epi == EPI_BIAS_GELU ? 32 : epi == EPI_GELU_BWD ? 32 : epi == EPI_ADD ? 48 : 16;
+}
+
+__device__ __forceinline__ void tile_of(int t, int ntn, int& m0, int& n0) {
+  m0 = (t / ntn) * BM;
+  n0 = (t % ntn) * BN;
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4, sw = li & 7;
+  const int wm = w >> 2, wn = w & 3;
+  const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn;
+  const int nk = g.K / BK;
+  // tile sequence of this workgroup: XCD group x gets tiles [beg, end), member l takes beg + l + 32 i
+  const int nwg = gridDim.x, x = blockIdx.x % 8, l = blockIdx.x / 8, per = nwg / 8;
+  const int q = ntiles / 8, r = ntiles % 8;
+  const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const int end = beg + q + (x < r ? 1 : 0);
+  int t = beg + l;
+  if (t >= end) return;   // more workgroups than tiles in this group (small problems)
+  int m0, n0;
+  tile_of(t, ntn, m0, n0);
+  const StageOffs so = stage_offsets(w, lane, g.lda, g.ldb);
+  auto rsa = uniform_rsrc(g.a + (size_t)m0 * g.lda), rsb = uniform_rsrc(g.b + (size_t)n0 * g.ldb);
+  stage<0>(so, rsa, rsb, smem, 0);
+  stage<1>(so, rsa, rsb, smem, 0);
+  stage<2>(so, rsa, rsb, smem, 0);
+  stage<3>(so, rsa, rsb, smem, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(wm) == 1) bar();   // stagger wave row 1
+
+  const int arow = (wm * 128 + li) * 128;
+  const int brow = A_BYTES + (wn * 64 + li) * 128;
+  const int ch0 = ((0 * 4 + lq) ^ sw) * 16, ch1 = ((1 * 4 + lq) ^ sw) * 16;
+  constexpr int S = kStores(EPI);
+  constexpr int WAIT_FIRST = 4 + S > 63 ? 63 : 4 + S;
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  f32x4 acc[8][4];
+  int buf = 0;
+  int it = 0;
+  STAMP_ID(0);
+  while (true) {
+    STAMP(0, it);
+    const int tn = t + per;
+    const bool has_next = tn < end;
+    int m1 = 0, n1 = 0;
+    if (has_next) tile_of(tn, ntn, m1, n1);
+    const auto rsa1 = uniform_rsrc(g.a + (size_t)m1 * g.lda), rsb1 = uniform_rsrc(g.b + (size_t)n1 * g.ldb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* cur = smem + buf * TILE_BYTES;
+      char* nxt = smem + (buf ^ 1) * TILE_BYTES;
+      buf ^= 1;
+      // what the phases of this K-step stage: the next K-step of this tile, else K-step 0 of the
+      // next tile, else nothing (the very last K-step)
+      const bool more_here = kt + 1 < nk;
+      const bool more = more_here || has_next;
+      const auto sra = more_here ? rsa : rsa1, srb = more_here ? rsb : rsb1;
+      const int skt = more_here ? kt + 1 : 0;
+      const bool first = kt == 0;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (p == 0 || p == 2) {
+          const int qm = p == 0 ? 0 : 1;
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) {
+            const char* rr = cur + arow + (qm * 4 + mi) * 16 * 128;
+            af[mi][0] = *reinterpret_cast<const bf16x8*>(rr + ch0);
+            af[mi][1] = *reinterpret_cast<const bf16x8*>(rr + ch1);
+          }
+        }
+        if (p == 0 || p == 1) {
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) {
+            const char* rr = cur + brow + (p * 2 + ni) * 16 * 128;
+            bf16x8 x0 = *reinterpret_cast<const bf16x8*>(rr + ch0);
+            bf16x8 x1 = *reinterpret_cast<const bf16x8*>(rr + ch1);
+            if (p == 0) { b0[ni][0] = x0; b0[ni][1] = x1; } else { b1[ni][0] = x0; b1[ni][1] = x1; }
+          }
+        }
+        if (more) {
+          if (p == 0) stage<0>(so, sra, srb, nxt, skt);
+          if (p == 1) stage<1>(so, sra, srb, nxt, skt);
+          if (p == 2) stage<2>(so, sra, srb, nxt, skt);
+          if (p == 3) stage<3>(so, sra, srb, nxt, skt);
+          if (first && p < 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WAIT_FIRST) : "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else if (p == 0) {
+          if (first) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WAIT_FIRST - 2) : "memory");
+          else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        const int qm = (p == 2 || p == 3) ? 1 : 0;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+              const bf16x8 bb = (p == 1 || p == 2) ? b1[ni][ks] : b0[ni][ks];
+              const int nn = ((p == 1 || p == 2) ? 2 : 0) + ni;
+              acc[qm * 4 + mi][nn] = mfma16(bb, af[mi][ks], acc[qm * 4 + mi][nn]);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        bar();
       }
-    if (li == 0) {
-      float* prow = g.part + (size_t)((m0 + wm * WM) / WM) * g.N + n0 + wn * 64 + 4 * lq;
+    }
+
+    STAMP(2, it);
+    // ---- epilogue through the free LDS buffer (the last K-step's; the other one holds the
+    //      next tile's K-step 0), in two rounds of 128 rows: the wave row r writes its
+    //      accumulators (fp32 bias / residual, one bf16 rounding) as a [128][512 B] image
+    //      (8-byte slots XOR-swizzled by row & 15), then all 8 waves store 16 rows each as
+    //      512-byte row segments of 16-byte vectors.
+    // accumulators -> packed bf16 first (fp32 bias / residual, one rounding): halves the live
+    // registers for the rest of the epilogue
+    bf16x4 pk[8][4];
+    if constexpr (EPI == EPI_ADD) {
+      const auto rs = uniform_rsrc(g.c + (size_t)(m0 + wm * 128) * g.ldc + n0 + wn * 64);
+      const int voff = (li * g.ldc + 4 * lq) * 2;
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        *reinterpret_cast<f32x4*>(prow + ni * 16) = f32x4{colsum[ni][0], colsum[ni][1], colsum[ni][2], colsum[ni][3]};
+      for (int h = 0; h < 2; ++h) {
+        bf16x4 cin[4][4];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            cin[mi][ni] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(
+                                                         rs, voff + ni * 32, (h * 4 + mi) * 16 * g.ldc * 2, 0));
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              pk[h * 4 + mi][ni][k] = (bf16)(acc[h * 4 + mi][ni][k] + (float)cin[mi][ni][k]);
+      }
+    } else {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (EPI == EPI_STORE || EPI == EPI_BIAS_GELU) {
+          if (g.bias) {
+            const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n0 + wn * 64 + ni * 16 + 4 * lq);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bv[k] = (float)b4[k];
+          }
+        }
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) pk[mi][ni][k] = (bf16)(acc[mi][ni][k] + bv[k]);
+      }
+    }
+    if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
+    bar();                                                // every wave is done with `img`
+    char* img = smem + (buf ^ 1) * TILE_BYTES;            // = the last K-step's buffer
+    const int c = lane & 31;
+    // row-phase inputs first (GELU_BWD: U), so no later load wait holds back a store
+    bf16x8 uin[2][8];
+    if constexpr (EPI == EPI_GELU_BWD) {
+      const auto rs = uniform_rsrc(g.u + (size_t)m0 * g.ldu + n0);
+      const int voff = ((w * 16 + (lane >> 5)) * g.ldu + c * 8) * 2;
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          uin[rr][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rs, voff, (rr * 128 + 2 * i) * g.ldu * 2, 0));
+    }
+    float colsum[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      if (__builtin_amdgcn_readfirstlane(wm) == rr) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int n = wn * 64 + ni * 16 + 4 * lq;
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi) {
+            const int m = mi * 16 + li;   // row within the round's 128
+            *reinterpret_cast<bf16x4*>(img + m * 512 + (((n >> 2) ^ (m & 15)) << 3)) = pk[mi][ni];
+          }
+        }
+      }
+      bar();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = w * 16 + 2 * i + (lane >> 5);   // row within the round
+        const int x = r & 15;
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(img + r * 512 + ((c ^ (x >> 1)) << 4));
+        if (x & 1) v = __builtin_shufflevector(v, v, 4, 5, 6, 7, 0, 1, 2, 3);
+        const size_t off = (size_t)(m0 + rr * 128 + r) * g.ldc + n0 + c * 8;
+        if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
+          *reinterpret_cast<bf16x8*>(g.c + off) = v;
+        } else if constexpr (EPI == EPI_BIAS_GELU) {
+          bf16x8 av;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) av[j] = (bf16)gelu((float)v[j]);
+          *reinterpret_cast<bf16x8*>(g.c + off) = v;
+          *reinterpret_cast<bf16x8*>(g.c2 + off) = av;
+        } else {
+          bf16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float du = (float)v[j] * gelu_grad((float)uin[rr][i][j]);
+            o[j] = (bf16)du;
+            colsum[j] += du;
+          }
+          *reinterpret_cast<bf16x8*>(g.c + off) = o;
+        }
+      }
+      bar();   // the image is consumed before it is rewritten / restaged
+    }
+    if constexpr (EPI == EPI_GELU_BWD) {
+      // lanes c and c+32 hold the same columns; the 8 waves combine through LDS: one fp32
+      // partial row per 256-row tile
+#pragma unroll
+      for (int j = 0; j < 8; ++j) colsum[j] += __shfl_xor(colsum[j], 32, 64);
+      float* red = reinterpret_cast<float*>(img);
+      if (lane < 32) {
+        *reinterpret_cast<f32x4*>(red + w * 256 + c * 8) = f32x4{colsum[0], colsum[1], colsum[2], colsum[3]};
+        *reinterpret_cast<f32x4*>(red + w * 256 + c * 8 + 4) = f32x4{colsum[4], colsum[5], colsum[6], colsum[7]};
+      }
+      bar();
+      if (tid < 256 && g.part) {
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum += red[k * 256 + tid];
+        g.part[(size_t)(m0 >> 8) * g.N + n0 + tid] = sum;
+      }
+      bar();
+    }
+    if (has_next && __builtin_amdgcn_readfirstlane(wm) == 1) bar();   // reopen the stagger
+    STAMP(4, it);
+    ++it;
+    if (!has_next) break;
+    t = tn;
+    m0 = m1;
+    n0 = n1;
+    rsa = rsa1;
+    rsb = rsb1;
+  }
+}
+
+// W [rows][cols] -> WT [cols][rows], bf16, 64 x 64 tiles through LDS (padded rows).  Vector form
+// (rows, cols multiples of 8): 16-byte global loads and stores; otherwise element-wise.
+__global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
+                                                             int rows, int cols) {
+  __shared__ bf16 tile[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, cc = c0 + tx;
+    if (r < rows && cc < cols) tile[i][tx] = in[(size_t)r * cols + cc];
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int cc = c0 + i, r = r0 + tx;
+    if (cc < cols && r < rows) out[(size_t)cc * rows + r] = tile[tx][i];
+  }
+}
+
+__global__ void __launch_bounds__(256) transpose_bf16_vec_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
+                                                                 int rows, int cols) {
+  __shared__ bf16 tile[64][72];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int t = threadIdx.x, cv = (t & 7) * 8, rv = t >> 3;   // 8 vectors per 64-wide row
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = rv + 32 * h;
+    if (r0 + r < rows && c0 + cv < cols) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(in + (size_t)(r0 + r) * cols + c0 + cv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tile[cv + j][r] = v[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int cc = rv + 32 * h;   // output row = input column
+    if (c0 + cc < cols && r0 + cv < rows) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = tile[cc][cv + j];
+      *reinterpret_cast<bf16x8*>(out + (size_t)(c0 + cc) * rows + r0 + cv) = v;
     }
   }
 }
 
 }  // namespace
 
-// Tile width: 256 (2 LDS stages) or 128 (3 stages, two K-steps in flight); DTD_GEMM_BN overrides.
-static int gemm_bn() {
-  static int bn = -1;
-  if (bn < 0) {
-    const char* e = getenv("DTD_GEMM_BN");
-    bn = e ? atoi(e) : 128;
-    if (bn != 128 && bn != 256) bn = 128;
+// Kernel form: 1 = persistent (default), 0 = one tile per workgroup with the LDS-image epilogue
+// (DTD_GEMM_VARIANT; kept for same-box A/B runs).
+static int gemm_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DTD_GEMM_VARIANT");
+    v = e ? atoi(e) : 1;
   }
-  return bn;
+  return v;
 }
 
-// Shape contract (checked): M % 256 == 0, N % gemm_bn() == 0, K % 64 == 0, lda/ldb/ldc/ldu % 8
-// == 0, 16-byte aligned base pointers.  part: [dtd_gemm_bt_part_rows(M)][N] fp32 (GELU_BWD
-// column partials, one row per wave row-block) or null.
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || c < 8)
+      c = 256;
+    n = c;
+  }
+  return n;
+}
+
+static unsigned long long* g_stamps = nullptr;
+// diagnostic builds: device buffer of [workgroups][32 tiles][8] u64 stamps (null: off)
+DTD_EXPORT int dtd_gemm_set_stamps(void* p) {
+  g_stamps = (unsigned long long*)p;
+  return 0;
+}
+
+// Shape contract (checked): M % 256 == 0, N % 256 == 0, K % 64 == 0, leading dimensions % 8 == 0,
+// 16-byte aligned base pointers (checked on the Python side).
 DTD_EXPORT int dtd_gemm_bt_supported(int M, int N, int K) {
-  return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % gemm_bn() == 0 && K % BK == 0;
+  return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0;
 }
 
-DTD_EXPORT int dtd_gemm_bt_part_rows(int M) { return M / (gemm_bn() == 256 ? 128 : 64); }
+// GELU_BWD column partials: one fp32 row per 256 rows of M
+DTD_EXPORT int dtd_gemm_bt_part_rows(int M) { return M / BM; }
 
 DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int ldb, void* c, int ldc, void* c2,
                            const void* u, int ldu, const void* bias, float* part, int M, int N, int K,
                            hipStream_t s) {
   if (!dtd_gemm_bt_supported(M, N, K)) return (int)hipErrorInvalidValue;
   if ((lda | ldb | ldc) % 8 || (u && ldu % 8)) return (int)hipErrorInvalidValue;
+  if (lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
   if (epi == EPI_BIAS_GELU && !c2) return (int)hipErrorInvalidValue;
   if (epi == EPI_GELU_BWD && !u) return (int)hipErrorInvalidValue;
-  GemmArgs g{(const bf16*)a, (const bf16*)b, (bf16*)c, ldc, (bf16*)c2, (const bf16*)u, ldu, (const bf16*)bias, part,
-             M, N, K, lda, ldb};
-  const int bn = gemm_bn();
-  const dim3 grid((M / BM) * (N / bn));
-#define DTD_GEMM_LAUNCH(E)                                                                        \
-  if (bn == 256) hipLaunchKernelGGL((gemm_bt_kernel<E, 256, 2>), grid, dim3(512), 0, s, g);     \
-  else hipLaunchKernelGGL((gemm_bt_kernel<E, 128, 3>), grid, dim3(512), 0, s, g)
+  GemmArgs g{(const bf16*)a, (const bf16*)b, (bf16*)c, (bf16*)c2, (const bf16*)u, (const bf16*)bias, part,
+             M, N, K, lda, ldb, ldc, ldu, g_stamps};
+  const int ntiles = (M / BM) * (N / BN);
+  if (gemm_variant() == 1) {
+    const int cus = num_cus() / 8 * 8;
+    const int nwg = ntiles >= cus ? cus : (ntiles + 7) / 8 * 8;
+#define DTD_GEMM_P(E) hipLaunchKernelGGL(gemm_bt_persistent<E>, dim3(nwg), dim3(512), 0, s, g)
+    switch (epi) {
+      case EPI_STORE: DTD_GEMM_P(EPI_STORE); break;
+      case EPI_BIAS_GELU: DTD_GEMM_P(EPI_BIAS_GELU); break;
+      case EPI_GELU_BWD: DTD_GEMM_P(EPI_GELU_BWD); break;
+      case EPI_ADD: DTD_GEMM_P(EPI_ADD); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+#undef DTD_GEMM_P
+    DTD_LAUNCH_CHECK();
+  }
+  const dim3 grid(ntiles);
   switch (epi) {
-    case EPI_STORE: DTD_GEMM_LAUNCH(EPI_STORE); break;
-    case EPI_BIAS_GELU: DTD_GEMM_LAUNCH(EPI_BIAS_GELU); break;
-    case EPI_GELU_BWD: DTD_GEMM_LAUNCH(EPI_GELU_BWD); break;
+    case EPI_STORE: hipLaunchKernelGGL(gemm_bt_kernel<EPI_STORE>, grid, dim3(512), 0, s, g); break;
+    case EPI_BIAS_GELU: hipLaunchKernelGGL(gemm_bt_kernel<EPI_BIAS_GELU>, grid, dim3(512), 0, s, g); break;
+    case EPI_GELU_BWD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_GELU_BWD>, grid, dim3(512), 0, s, g); break;
+    case EPI_ADD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_ADD>, grid, dim3(512), 0, s, g); break;
     default: return (int)hipErrorInvalidValue;
   }
-#undef DTD_GEMM_LAUNCH
+  DTD_LAUNCH_CHECK();
+}
+
+DTD_EXPORT int dtd_transpose_bf16(const void* in, void* out, int rows, int cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  if (rows % 8 == 0 && cols % 8 == 0 && ((uintptr_t)in | (uintptr_t)out) % 16 == 0)
+    hipLaunchKernelGGL(transpose_bf16_vec_kernel, grid, dim3(256), 0, s, (const bf16*)in, (bf16*)out, rows, cols);
+  else
+    hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, s, (const bf16*)in, (bf16*)out, rows, cols);
   DTD_LAUNCH_CHECK();
 }

@@ -1,50 +1,77 @@
-"""Hand-written MFMA GEMM with fused FFN epilogues (``ops/csrc/gemm.hip``).
+"""Hand-written MFMA GEMM with fused transformer epilogues (``ops/csrc/gemm.hip``).
 
-``C = A . B^T`` with both operands K-contiguous (a Linear weight [out, in] is exactly B):
+``C = A . B^T`` with both operands K-contiguous (a Linear weight [out, in] is exactly B; the
+input-gradient product uses the transposed weight, ``transpose``):
 
-* ``linear_gelu(x, w, b)``   -> (u, a): u = x W^T + b, a = gelu(u); the up-projection of the FFN
-  forward with the activation computed in the GEMM epilogue (no re-read of u).
-* ``gelu_bwd_gemm(dy, w_t, u, dbias)`` -> du = (dy . w_t^T) * gelu'(u) plus the column sums of du
-  (the up-projection's bias gradient); the FFN backward's down-projection dgrad with the GELU
-  derivative applied in the epilogue (no round trip of da through HBM).
-* ``gemm_bt(a, b, bias)``    -> plain product (tests / benchmarks).
+* ``linear(x, w, b)``              -> x W^T + b                      (Linear forward)
+* ``linear_gelu(x, w, b)``         -> (u, a): u = x W^T + b, a = gelu(u) computed in the epilogue
+                                      (FFN up-projection: no separate activation pass over u)
+* ``matmul_nt(a, b_t)``            -> a b_t^T                        (dgrad with b_t = W^T)
+* ``matmul_nt_add_(c, a, b_t)``    -> c += a b_t^T in place          (residual-branch dgrad)
+* ``gelu_bwd_gemm(dy, w_t, u, dbias)`` -> du = (dy w_t^T) * gelu'(u) plus the column sums of du
+                                      (FFN down-projection dgrad with the GELU derivative and the
+                                      up-projection's bias gradient in the epilogue)
 
-Status (measured on MI355X, ``scripts/bench_gemm_fused.py``, profiles/r1_gemm_fused_vs_hipblaslt.jsonl):
-the main loop reaches 630-660 TF/s at the FFN shape vs hipBLASLt's 940-970 on the same box, so
-the fused epilogues do not yet beat hipBLASLt + the bandwidth-bound activation kernels and the
-model keeps the unfused path; the kernels are tested building blocks for the deeper-pipelined
-(8-phase, cdna_hip_programming.md §5) main loop they need.
-
-Shapes must tile by 256 x 128 x 64 (256 x 256 x 64 with DTD_GEMM_BN=256) (``supported``); callers fall back to hipBLASLt + the
-elementwise kernels otherwise.  bf16 only.
+The kernel is the 256x256 8-phase LDS-DMA pipeline of cdna_hip_programming.md §5 (see the .hip
+header).  Shapes must tile by 256 x 256 x 64 (``supported``); callers fall back to hipBLASLt +
+the elementwise kernels otherwise.  bf16 only.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 from . import _lib
 
-EPI_STORE, EPI_BIAS_GELU, EPI_GELU_BWD = 0, 1, 2
+EPI_STORE, EPI_BIAS_GELU, EPI_GELU_BWD, EPI_ADD = 0, 1, 2, 3
+
+# DTD_GEMM=0 keeps every product on hipBLASLt (A/B runs); the model path checks ``enabled()``.
+_ENABLED = [os.environ.get("DTD_GEMM", "1") == "1"]
+
+
+# Which model products take the kernel (same-box A/B switches): the FFN up-projection forward with
+# the GELU epilogue, and the FFN down-projection dgrad with the GELU-backward epilogue.
+_FFN_FWD = [os.environ.get("DTD_GEMM_FFN_FWD", "1") == "1"]
+_FFN_BWD = [os.environ.get("DTD_GEMM_FFN_BWD", "1") == "1"]
+
+
+def enabled() -> bool:
+    return _ENABLED[0]
+
+
+def ffn_fwd_enabled() -> bool:
+    return _ENABLED[0] and _FFN_FWD[0]
+
+
+def ffn_bwd_enabled() -> bool:
+    return _ENABLED[0] and _FFN_BWD[0]
+
+
+def set_enabled(on: bool) -> None:
+    _ENABLED[0] = bool(on)
+
+
+def _ok(t: torch.Tensor) -> bool:
+    return (t is not None and t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1
+            and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0)
 
 
 def supported(M: int, N: int, K: int, *tensors) -> bool:
-    if not all(t is not None and t.is_cuda and t.dtype == torch.bfloat16 for t in tensors):
+    if not all(_ok(t) for t in tensors):
         return False
     if not _lib.has("dtd_gemm_bt"):
         return False
     return bool(_lib.lib().dtd_gemm_bt_supported(M, N, K))
 
 
-def _ld(t: torch.Tensor) -> int:
-    assert t.dim() == 2 and t.stride(1) == 1, "operands must be row-major with unit inner stride"
-    return t.stride(0)
-
-
 def _call(epi, a, b, c, c2=None, u=None, bias=None, part=None):
     M, K = a.shape
     N = b.shape[0]
-    _lib.call("dtd_gemm_bt", epi, a.data_ptr(), _ld(a), b.data_ptr(), _ld(b), c.data_ptr(), _ld(c), _lib.ptr(c2),
-              _lib.ptr(u), _ld(u) if u is not None else 0, _lib.ptr(bias), _lib.ptr(part), M, N, K, _lib.stream())
+    assert b.shape[1] == K and c.shape == (M, N), (a.shape, b.shape, c.shape)
+    _lib.call("dtd_gemm_bt", epi, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+              _lib.ptr(c2), _lib.ptr(u), u.stride(0) if u is not None else 0, _lib.ptr(bias), _lib.ptr(part),
+              M, N, K, _lib.stream())
 
 
 def gemm_bt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
@@ -53,8 +80,23 @@ def gemm_bt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None) 
     return c
 
 
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    return gemm_bt(x, w, b)
+
+
+def matmul_nt(a: torch.Tensor, b_t: torch.Tensor) -> torch.Tensor:
+    return gemm_bt(a, b_t)
+
+
+def matmul_nt_add_(c: torch.Tensor, a: torch.Tensor, b_t: torch.Tensor) -> torch.Tensor:
+    """c += a . b_t^T (fp32 sum of the product and c, one bf16 rounding)."""
+    _call(EPI_ADD, a, b_t, c)
+    return c
+
+
 def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None):
-    """(u, a) = (x W^T + b, gelu(u)) in one kernel."""
+    """(u, a) = (x W^T + b, gelu(u)) in one kernel (GELU of the stored bf16 u, as the unfused
+    activation kernel computes it)."""
     M, N = x.shape[0], w.shape[0]
     u = torch.empty((M, N), dtype=x.dtype, device=x.device)
     a = torch.empty_like(u)
@@ -62,15 +104,26 @@ def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None):
     return u, a
 
 
-def gelu_bwd_gemm(dy: torch.Tensor, w_t: torch.Tensor, u: torch.Tensor, dbias=None, acc: bool = False):
-    """du = (dy . w_t^T) * gelu'(u); ``w_t`` is the down-projection weight transposed to
+def gelu_bwd_gemm(dy: torch.Tensor, w_t: torch.Tensor, u: torch.Tensor, dbias=None):
+    """du = bf16(dy . w_t^T) * gelu'(u); ``w_t`` is the down-projection weight transposed to
     [ffn, hidden] (K-contiguous).  ``dbias`` (dst, acc) receives the column sums of du."""
     from .functional import _finalize
     M, N = dy.shape[0], w_t.shape[0]
     du = torch.empty((M, N), dtype=dy.dtype, device=dy.device)
-    nrows = _lib.lib().dtd_gemm_bt_part_rows(M)
-    part = torch.empty((nrows, N), dtype=torch.float32, device=dy.device) if dbias is not None else None
+    part = None
+    if dbias is not None:
+        nrows = _lib.lib().dtd_gemm_bt_part_rows(M)
+        part = torch.empty((nrows, N), dtype=torch.float32, device=dy.device)
     _call(EPI_GELU_BWD, dy, w_t, du, u=u, part=part)
     if part is not None:
-        _finalize(part, nrows, N, dbias, acc)
+        dst, acc = dbias
+        _finalize(part, part.shape[0], N, (dst, acc), acc)
     return du
+
+
+def transpose(w: torch.Tensor) -> torch.Tensor:
+    """w^T as a new contiguous bf16 tensor (LDS-tiled transpose kernel)."""
+    assert w.dim() == 2 and w.is_contiguous() and w.dtype == torch.bfloat16
+    out = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+    _lib.call("dtd_transpose_bf16", w.data_ptr(), out.data_ptr(), w.shape[0], w.shape[1], _lib.stream())
+    return out

@@ -72,6 +72,8 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "attn_occ_322": _env(DTD_ATTN_OCC="3,2,2"), "attn_occ_323_dq64": _env(DTD_ATTN_OCC="3,2,3", DTD_ATTN_TILE="64,64"),
            "base": lambda: None, "old_wgrad_split": _old_wgrad_split, "f32_wgrad_partials": _f32_wgrad_partials,
            "no_keep_ffn_act": _no_keep_ffn_act, "ew_plain": _env(DTD_EW_MODE="0"),
+           "no_gemm": _env(DTD_GEMM="0"), "gemm_bwd_only": _env(DTD_GEMM_FFN_FWD="0"),
+           "gemm_fwd_only": _env(DTD_GEMM_FFN_BWD="0"), "gemm_tile": _env(DTD_GEMM_VARIANT="0"),
            "base_so": _env(DTD_KERNELS_SO=os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops",
                                                       "_dtd_kernels_base.so"))}
 

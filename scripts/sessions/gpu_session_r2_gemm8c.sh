@@ -1,0 +1,11 @@
+#!/usr/bin/env bash
+# Persistent GEMM with the two-round LDS epilogue: tests, probe, stamps, model-shape A/B.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+source scripts/gpu_step.sh
+export TMPDIR=/tmp
+step gemm_tests_p 300 python -u -m pytest tests/test_gemm_gpu.py -x -v --timeout 120 --timeout-method thread
+grep -q " passed" gpurun_out/gemm_tests_p.log && ! grep -q "failed" gpurun_out/gemm_tests_p.log || exit 1
+step probe_p 300 python -u scripts/gemm_probe.py
+DTD_GEMM_VARIANT=1 step stamps_p 200 python -u scripts/gemm_stamps.py
+step gemm_bench_p 400 python -u scripts/bench_gemm8.py
+echo done

@@ -13,7 +13,8 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 768), (1024, 3072, 768), (768, 768, 3072)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 192), (512, 768, 768), (1024, 3072, 768),
+                                   (768, 768, 3072), (512, 768, 2304)])
 def test_gemm_bt_matches_fp32(M, N, K):
     torch.manual_seed(0)
     a = torch.randn(M, K, device="cuda").bfloat16()
@@ -65,3 +66,31 @@ def test_gelu_bwd_gemm_epilogue_and_bias_grad():
     xg = u.float()
     g = 0.5 * (1 + torch.erf(xg / 2 ** 0.5)) + xg * torch.exp(-0.5 * xg * xg) / (2 * torch.pi) ** 0.5
     assert rel(du, (dy.float() @ w2.float()) * g) < 2e-2
+
+
+def test_gemm_nt_add_in_place_and_transpose():
+    torch.manual_seed(3)
+    M, N, K = 512, 768, 2304
+    dy = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(K, N, device="cuda") * 0.05).bfloat16()          # qkv weight [out=K, in=N]
+    wt = G.transpose(w)
+    assert torch.equal(wt, w.t().contiguous())
+    c = torch.randn(M, N, device="cuda").bfloat16()
+    ref = c.float() + dy.float() @ w.float()
+    G.matmul_nt_add_(c, dy, wt)
+    assert rel(c, ref) < 1e-2, rel(c, ref)
+    # odd transpose shapes (tile edges)
+    x = torch.randn(100, 37, device="cuda").bfloat16()
+    assert torch.equal(G.transpose(x), x.t().contiguous())
+
+
+def test_gemm_strided_operands_and_many_tiles():
+    """Row-strided views (lda > K) and a grid that is not a multiple of the 8 XCDs."""
+    torch.manual_seed(4)
+    M, N, K = 256 * 5, 256 * 3, 128
+    big = torch.randn(M, K + 64, device="cuda").bfloat16()
+    a = big[:, :K]
+    b = torch.randn(N, K, device="cuda").bfloat16()
+    assert G.supported(M, N, K, a, b)
+    c = G.gemm_bt(a, b)
+    assert rel(c, a.float() @ b.float().t()) < 1e-2
