@@ -65,8 +65,14 @@ def init(rank: int | None = None, world_size: int | None = None, backend: str | 
 
 
 def destroy() -> None:
+    """Orderly teardown: every rank reaches the barrier before any rank closes its transport.
+    (Without it a fast rank's exit can close gloo pairs under a peer that is still finishing
+    its last collective; that peer's transport thread then aborts the process.)"""
     if dist.is_initialized():
-        dist.destroy_process_group()
+        try:
+            dist.barrier()
+        finally:
+            dist.destroy_process_group()
 
 
 def rank() -> int:

@@ -5,9 +5,11 @@
 with ``seed + epoch`` (shuffle=True default), padded by repetition to a multiple of the world
 size (drop_last=False), then ``indices[rank::world]``.
 
-``DeviceBatchLoader`` replaces the DataLoader hot path: it gathers a whole batch with one
-index_select on pinned host memory and issues a single non-blocking H2D copy per tensor on a
-side stream (double-buffered), so the input copy overlaps the previous step's compute.
+``DeviceBatchLoader`` replaces the DataLoader hot path: the native worker pool
+(``runtime/csrc/loader.cpp``) gathers a whole batch's rows straight into one of two reused
+pinned host slots, and a single non-blocking H2D copy per tensor runs on a side stream, one
+batch ahead, so the input copy overlaps the previous step's compute.  Datasets that produce rows
+on demand (``NativeSyntheticLM``) are generated into the slot by the same workers instead.
 """
 from __future__ import annotations
 
@@ -62,16 +64,22 @@ class DistributedSampler(torch.utils.data.Sampler):
 class DeviceBatchLoader:
     """Iterate fixed-size batches of a tensor dataset directly onto a device."""
 
+    SLOTS = 2
+
     def __init__(self, dataset, batch_size: int, sampler=None, device="cpu", drop_last: bool = False,
-                 keys=("input_ids", "labels")):
+                 keys=("input_ids", "labels"), threads: int = 0):
+        from ..runtime import BatchProducer
         self.dataset, self.batch_size, self.device = dataset, batch_size, torch.device(device)
         self.sampler = sampler if sampler is not None else range(len(dataset))
         self.drop_last, self.keys = drop_last, keys
-        pin = self.device.type == "cuda"
-        self._host = {k: getattr(dataset, k) for k in keys}
-        if pin:
-            self._host = {k: v.pin_memory() for k, v in self._host.items()}
-        self._stream = torch.cuda.Stream(self.device) if pin else None
+        self._pin = self.device.type == "cuda"
+        self._generate = hasattr(dataset, "fill_rows")           # on-demand rows (NativeSyntheticLM)
+        self._host = {} if self._generate else {k: getattr(dataset, k).contiguous() for k in keys}
+        self._producer = BatchProducer(threads)
+        self._stream = torch.cuda.Stream(self.device) if self._pin else None
+        self._slots: list = []        # per slot: {key: pinned [batch, ...] tensor}
+        self._slot_ev: list = []      # per slot: event of the H2D copy that last read it
+        self._next_slot = 0
 
     def __len__(self):
         n = len(self.sampler)
@@ -85,16 +93,52 @@ class DeviceBatchLoader:
                 return
             yield torch.as_tensor(chunk, dtype=torch.int64)
 
+    def _host_slot(self, n: int):
+        """A pinned slot for an n-row batch whose previous H2D copy has finished."""
+        k = self._next_slot
+        self._next_slot = (k + 1) % self.SLOTS
+        if len(self._slots) <= k:
+            self._slots.append({})
+            self._slot_ev.append(None)
+        if self._slot_ev[k] is not None:
+            self._slot_ev[k].synchronize()
+            self._slot_ev[k] = None
+        slot = self._slots[k]
+        for key in self.keys:
+            t = slot.get(key)
+            shape = (n,) + self._row_shape(key)
+            if t is None or t.shape != shape:
+                t = torch.empty(shape, dtype=self._dtype(key), pin_memory=self._pin)
+                slot[key] = t
+        return k, slot
+
+    def _row_shape(self, key):
+        return tuple(self.dataset.row_shape(key)) if self._generate else tuple(self._host[key].shape[1:])
+
+    def _dtype(self, key):
+        return self.dataset.row_dtype(key) if self._generate else self._host[key].dtype
+
     def _load(self, ix):
+        n = ix.numel()
+        if self._pin:
+            k, host = self._host_slot(n)
+        else:
+            k, host = None, {key: torch.empty((n,) + self._row_shape(key), dtype=self._dtype(key)) for key in self.keys}
+        if self._generate:
+            self.dataset.fill_rows(ix, host, self._producer)
+        else:
+            jobs = [self._producer.gather(self._host[key], ix, host[key][:n], wait=False) for key in self.keys]
+            for j in jobs:
+                self._producer.wait(j)
+        if not self._pin:
+            return {key: v.to(self.device) for key, v in host.items()}
         out = {}
-        for k, v in self._host.items():
-            b = v.index_select(0, ix)
-            if self._stream is not None:
-                b = b.pin_memory()
-                with torch.cuda.stream(self._stream):
-                    out[k] = b.to(self.device, non_blocking=True)
-            else:
-                out[k] = b.to(self.device)
+        with torch.cuda.stream(self._stream):
+            for key, v in host.items():
+                out[key] = v.to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(self._stream)
+        self._slot_ev[k] = ev     # the slot is reused only after this copy has read it
         return out
 
     def __iter__(self):

@@ -57,7 +57,10 @@ def note_use(params) -> None:
     if not _COUNTING[0] or not torch.is_grad_enabled():
         return
     for p in params:
-        if getattr(p, "_dtd_ready_hook", None) is not None:
+        exp = getattr(p, "_dtd_expect", None)
+        if exp is not None:          # owner counts in the native tracker (runtime/)
+            exp(p)
+        elif getattr(p, "_dtd_ready_hook", None) is not None:
             p._dtd_pending = getattr(p, "_dtd_pending", 0) + 1
 
 

@@ -13,6 +13,10 @@ reducer:
   bucket is all-reduced immediately (``async_op``: RCCL runs on its own stream and waits on
   the compute stream's event), in bucket-index order on every rank, so communication overlaps
   the remaining backward.  ``finish`` makes the compute stream wait for all buckets.
+* The bookkeeping -- bucket assignment, per-parameter expected-contribution counts, bucket
+  completeness and the in-order launch decisions -- runs in the native C++ tracker
+  (``runtime/csrc/reducer.cpp``, the counterpart of torch's C++ Reducer); Python issues the
+  collectives it asks for.
 * RCCL averages in the collective (``ReduceOp.AVG``); gloo (CPU tests) sums then scales.
 * Gradients can be kept/communicated in bf16 (``grad_dtype``): half the xGMI bytes of the
   reference's fp32 buckets.  Bucket size defaults to the reference's 25 MiB; on an 8-GPU
@@ -35,6 +39,7 @@ from torch import nn
 from ..comm import logger as comm_log
 from ..ops.grad import join_async_wgrad, set_async_wgrad
 from ..ops.grad import _ASYNC as _ASYNC_WGRAD
+from ..runtime import ReadyTracker, assign_buckets
 from .flat import FlatLayout, GradBuffer
 
 
@@ -43,12 +48,10 @@ def wgrad_stream(device) -> torch.cuda.Stream:
 
 
 class _Bucket:
-    __slots__ = ("index", "start", "end", "params", "ready", "launched", "work")
+    __slots__ = ("index", "start", "end", "params", "work")
 
     def __init__(self, index, start, end, params):
         self.index, self.start, self.end, self.params = index, start, end, params
-        self.ready = set()
-        self.launched = False
         self.work = None
 
 
@@ -79,10 +82,13 @@ class DistributedDataParallel(nn.Module):
         self.device = p0.device
         self.param_flat = self.layout.flatten_params_() if flatten_params else None
         self.grad_dtype = grad_dtype or p0.dtype
-        self.grads = GradBuffer(self.layout, self.grad_dtype, self.device, on_ready=self._on_ready)
+        self.grads = GradBuffer(self.layout, self.grad_dtype, self.device, on_contribution=self._on_contribution)
         self._build_buckets(bucket_cap_mb)
+        for p in self.layout.params:
+            p._dtd_expect = self._expect
         self._sync_enabled = True
         self._need_reset = True
+        self._window_open = False
         self._callback_queued = False
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
         self._xgmi = None
@@ -110,19 +116,12 @@ class DistributedDataParallel(nn.Module):
     def _build_buckets(self, cap_mb: float) -> None:
         cap = int(cap_mb * 1024 * 1024 / self.grads.buf.element_size())
         L = self.layout
-        self.buckets, cur, start = [], [], 0
-        for i, p in enumerate(L.params):
-            s, _ = L.offsets[i], None
-            if cur and (s - start) + p.numel() > cap:
-                self.buckets.append(_Bucket(len(self.buckets), start, s, cur))
-                cur, start = [], s
-            cur.append(p)
-        end = L.numel
-        self.buckets.append(_Bucket(len(self.buckets), start, end, cur))
-        self._bucket_of = {}
-        for b in self.buckets:
-            for p in b.params:
-                self._bucket_of[id(p)] = b
+        bucket_of, ranges = assign_buckets(L.offsets, [p.numel() for p in L.params], L.numel, cap)
+        members = [[] for _ in ranges]
+        for i, b in enumerate(bucket_of):
+            members[b].append(L.params[i])
+        self.buckets = [_Bucket(k, s, e, members[k]) for k, (s, e) in enumerate(ranges)]
+        self.tracker = ReadyTracker(bucket_of, len(self.buckets))
 
     @torch.no_grad()
     def _broadcast_params(self) -> None:
@@ -136,8 +135,6 @@ class DistributedDataParallel(nn.Module):
     def _reset(self) -> None:
         self.grads.reset()
         for b in self.buckets:
-            b.ready.clear()
-            b.launched = False
             b.work = None
         self._callback_queued = False
         self._need_reset = False
@@ -145,6 +142,9 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *args, **kwargs):
         if self._need_reset:
             self._reset()
+        if not self._window_open:   # a new backward window: fresh readiness / launch state
+            self.tracker.reset()
+            self._window_open = True
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager
@@ -157,27 +157,21 @@ class DistributedDataParallel(nn.Module):
         finally:
             self._sync_enabled = prev
 
-    def _on_ready(self, p) -> None:
+    def _expect(self, p) -> None:
+        self.tracker.expect(self.layout.index[id(p)])
+
+    def _on_contribution(self, p, autograd: bool) -> None:
         if not self._callback_queued:
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finish_backward)
-        if not (self._sync_enabled and self.overlap):
-            return
-        b = self._bucket_of[id(p)]
-        b.ready.add(id(p))
-        if len(b.ready) == len(b.params):
-            self._launch_ready_in_order()
-
-    def _launch_ready_in_order(self) -> None:
-        for b in self.buckets:
-            if b.launched:
-                continue
-            if len(b.ready) < len(b.params):
-                return  # keep the collective order identical on every rank
-            self._launch(b)
+        # the tracker launches complete buckets in bucket order only (identical collective
+        # sequence on every rank); inside no_sync it just counts
+        _, launch = self.tracker.contribute(self.layout.index[id(p)], autograd,
+                                            allow_launch=self._sync_enabled and self.overlap)
+        for k in launch:
+            self._launch(self.buckets[k])
 
     def _launch(self, b: _Bucket) -> None:
-        b.launched = True
         if self.world == 1:
             return
         view = self.grads.buf[b.start:b.end]
@@ -202,6 +196,7 @@ class DistributedDataParallel(nn.Module):
         # one end-of-backward callback per backward pass, synced or not: the next backward
         # (e.g. the synced micro-step after a no_sync one) must queue its own
         self._callback_queued = False
+        self._window_open = False
         if not self._sync_enabled:
             return
         self.finish()
@@ -212,9 +207,9 @@ class DistributedDataParallel(nn.Module):
         if self.async_wgrad:
             join_async_wgrad(self.device)
         self.grads.zero_untouched_()
-        for b in self.buckets:
-            if not b.launched:
-                self._launch(b)
+        for k in self.tracker.drain():
+            self._launch(self.buckets[k])
+        self._window_open = False
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()

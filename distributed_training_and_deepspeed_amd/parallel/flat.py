@@ -71,13 +71,16 @@ class GradBuffer:
     ``on_ready(p)`` (optional) is called once per parameter per backward when all of its
     expected contributions have arrived (fused modules announce uses in forward via
     ``ops.grad.note_use``; autograd-path parameters contribute once, through a
-    post-accumulate-grad hook that folds ``p.grad`` into ``main_grad``)."""
+    post-accumulate-grad hook that folds ``p.grad`` into ``main_grad``).
+    ``on_contribution(p, autograd)`` (optional) replaces that counting: every contribution is
+    handed to the owner (the DDP reducer counts them in the native tracker, runtime/)."""
 
-    def __init__(self, layout: FlatLayout, dtype: torch.dtype, device, on_ready=None):
+    def __init__(self, layout: FlatLayout, dtype: torch.dtype, device, on_ready=None, on_contribution=None):
         self.layout = layout
         self.dtype = dtype
         self.buf = torch.zeros(layout.numel, dtype=dtype, device=device)
         self.on_ready = on_ready
+        self.on_contribution = on_contribution
         self._hooks = []
         for i, p in enumerate(layout.params):
             p.main_grad = layout.view(self.buf, i)
@@ -101,6 +104,9 @@ class GradBuffer:
         self._ready(p, autograd=True)
 
     def _ready(self, p, autograd: bool = False):
+        if self.on_contribution is not None:
+            self.on_contribution(p, autograd)
+            return
         pend = getattr(p, "_dtd_pending", 0)
         if pend > 0 and not autograd:
             pend -= 1
@@ -133,6 +139,6 @@ class GradBuffer:
         for h in self._hooks:
             h.remove()
         for p in self.layout.params:
-            for a in ("main_grad", "_dtd_ready_hook", "_dtd_touched", "_dtd_pending"):
+            for a in ("main_grad", "_dtd_ready_hook", "_dtd_touched", "_dtd_pending", "_dtd_expect"):
                 if hasattr(p, a):
                     delattr(p, a)

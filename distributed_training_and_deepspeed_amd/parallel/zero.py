@@ -40,6 +40,7 @@ from torch import nn
 from .. import comm
 from ..comm import logger as clog
 from ..optim.fused_adam import FusedAdam
+from ..runtime import ReadyTracker
 from .flat import ALIGN, unique_params
 
 DEFAULTS = {
@@ -169,9 +170,17 @@ class ZeroEngine(nn.Module):
             off += s.chunk
         self.shard_numel = off
         self._seg_of = {}
+        self._pindex = {}
+        bucket_of = []
         for s in self.segments:
             for i, p in enumerate(s.params):
                 self._seg_of[id(p)] = (s, i)
+                self._pindex[id(p)] = len(bucket_of)
+                bucket_of.append(s.index)
+        # native readiness tracker (runtime/csrc/reducer.cpp): expected-contribution counts per
+        # parameter, segment completeness, in-order launch of the reduce buckets; stage-3 units
+        # reduce as soon as they are complete
+        self.tracker = ReadyTracker(bucket_of, len(self.segments), ordered=[not s.unit for s in self.segments])
 
         self._broadcast_initial(params)
         self._build_storage()
@@ -290,6 +299,7 @@ class ZeroEngine(nn.Module):
         for s in self.segments:
             for p in s.params:
                 p._dtd_ready_hook = self._on_ready
+                p._dtd_expect = self._expect
                 p._dtd_touched = False
                 p._dtd_pending = 0
                 if self.stage >= 2 or s.unit:
@@ -322,33 +332,21 @@ class ZeroEngine(nn.Module):
             p.main_grad = s.view(s.gbuf, i)
             p._dtd_touched = False
 
+    def _expect(self, p) -> None:
+        self.tracker.expect(self._pindex[id(p)])
+
     def _on_ready(self, p, autograd: bool = False) -> None:
         if not self._callback_queued:
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
-        pend = getattr(p, "_dtd_pending", 0)
-        if pend > 0 and not autograd:
-            pend -= 1
-            p._dtd_pending = pend
-            if pend > 0:
-                return
-        s, _ = self._seg_of[id(p)]
-        s.ready += 1
-        if self.stage <= 1 and not self.is_gradient_accumulation_boundary():
-            return
-        if s.ready == len(s.params) and self.config.overlap:
+        allow = self.config.overlap and not (self.stage <= 1 and not self.is_gradient_accumulation_boundary())
+        _, launch = self.tracker.contribute(self._pindex[id(p)], autograd, allow_launch=allow)
+        for k in launch:
+            s = self.segments[k]
             if s.unit:
                 self._reduce_unit(s)
-            else:
-                self._launch_ready_buckets_in_order()
-
-    def _launch_ready_buckets_in_order(self) -> None:
-        for s in self.buckets:
-            if s.launched:
-                continue
-            if s.ready < len(s.params):
-                return
-            self._reduce_segment(s)
+            elif not s.launched:
+                self._reduce_segment(s)
 
     def _comm_ctx(self):
         if self.comm_stream is None:
@@ -503,8 +501,8 @@ class ZeroEngine(nn.Module):
     # ================================================================== engine API
     def _reset(self) -> None:
         accumulate_full = self.stage <= 1 and self.micro_step > 0  # keep accumulating in place
+        self.tracker.reset()
         for s in self.segments:
-            s.ready = 0
             s.launched = False
             for p in s.params:
                 if not accumulate_full:

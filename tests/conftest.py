@@ -23,11 +23,15 @@ def pytest_collection_modifyitems(config, items):
             it.add_marker(skip)
 
 
-@pytest.fixture
-def free_port():
+def pick_free_port() -> int:
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     return port
+
+
+@pytest.fixture
+def free_port():
+    return pick_free_port()

@@ -84,7 +84,9 @@ def test_zero_stages_agree(tmp_path, free_port):
     world, steps, gas = 2, 3, 2
     results = {}
     for stage in (0, 1, 2, 3):
-        _spawn(W.zero_worker, world, free_port + stage, str(tmp_path), "causal-tiny", stage, steps, gas)
+        # a fresh port per rendezvous (free_port + k can collide with sockets of earlier tests)
+        from .conftest import pick_free_port
+        _spawn(W.zero_worker, world, pick_free_port(), str(tmp_path), "causal-tiny", stage, steps, gas)
         results[stage] = torch.load(tmp_path / f"zero{stage}.pt", weights_only=True)
     n_params = sum(p.numel() for p in build_model("causal-tiny").parameters())
     # stage 0 replicates; stages >= 1 hold 1/world of the (padded) optimizer state

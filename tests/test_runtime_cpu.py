@@ -1,0 +1,136 @@
+"""Native host runtime (runtime/csrc): readiness tracker, bucket assignment, batch producer."""
+import random
+
+import pytest
+import torch
+
+from distributed_training_and_deepspeed_amd.data import (DeviceBatchLoader, DistributedSampler, IGNORE_INDEX,
+                                                         NativeSyntheticLM)
+from distributed_training_and_deepspeed_amd.models import config as C
+from distributed_training_and_deepspeed_amd.runtime import BatchProducer, ReadyTracker, assign_buckets
+
+
+def test_tracker_launches_complete_buckets_in_order():
+    # params 0,1 -> bucket 0; 2,3 -> bucket 1; 4 -> bucket 2
+    t = ReadyTracker([0, 0, 1, 1, 2], 3)
+    t.reset()
+    assert t.contribute(2) == (True, [])
+    assert t.contribute(3) == (True, [])          # bucket 1 complete, but bucket 0 is not
+    assert t.contribute(4) == (True, [])
+    assert t.contribute(0) == (True, [])
+    ready, launch = t.contribute(1)
+    assert ready and launch == [0, 1, 2]             # the whole chain, in order
+    assert t.drain() == []
+    assert t.stats()["launches"] == 3
+
+
+def test_tracker_counts_expected_contributions_and_autograd_is_final():
+    t = ReadyTracker([0, 0], 1)
+    t.reset()
+    t.expect(0)
+    t.expect(0)                                      # a tied weight: two fused uses
+    assert t.contribute(0) == (False, [])
+    assert t.contribute(1, autograd=True) == (True, [])
+    ready, launch = t.contribute(0)
+    assert ready and launch == [0]
+    # readiness is idempotent inside a window; a reset opens a new one
+    assert t.contribute(1, autograd=True) == (True, [])
+    t.reset()
+    assert not t.is_ready(0) and not t.is_launched(0)
+
+
+def test_tracker_no_launch_window_then_drain():
+    t = ReadyTracker([0, 1, 1], 2)
+    t.reset()
+    for p in range(3):
+        assert t.contribute(p, allow_launch=False) == (True, [])
+    assert t.drain() == [0, 1]
+    assert t.is_launched(0) and t.is_launched(1)
+
+
+def test_tracker_eager_unit_buckets():
+    # bucket 0, 1 ordered; bucket 2 an eager unit (ZeRO-3)
+    t = ReadyTracker([0, 1, 2, 2], 3, ordered=[True, True, False])
+    t.reset()
+    t.contribute(2)
+    assert t.contribute(3) == (True, [2])            # launches although bucket 0 is incomplete
+    assert t.contribute(1) == (True, [])
+    assert t.contribute(0) == (True, [0, 1])
+
+
+def test_bucket_assign_matches_greedy_rule():
+    rng = random.Random(0)
+    for _ in range(50):
+        n = rng.randint(1, 40)
+        numels = [rng.randint(1, 5000) for _ in range(n)]
+        offsets, off = [], 0
+        for x in numels:
+            offsets.append(off)
+            off += -(-x // 64) * 64
+        cap = rng.randint(64, 20000)
+        bucket_of, ranges = assign_buckets(offsets, numels, off, cap)
+        # python reference of DDP's greedy rule
+        ref, cur, start = [], 0, 0
+        starts = [0]
+        for i in range(n):
+            if i and (offsets[i] - start) + numels[i] > cap and ref and ref[-1] == cur:
+                cur += 1
+                start = offsets[i]
+                starts.append(start)
+            ref.append(cur)
+        assert bucket_of == ref
+        assert [s for s, _ in ranges] == starts and ranges[-1][1] == off
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_producer_gather_matches_index_select(threads):
+    p = BatchProducer(threads)
+    src = torch.randint(0, 1000, (97, 33), dtype=torch.int64)
+    idx = torch.randint(0, 97, (50,))
+    dst = torch.empty(50, 33, dtype=torch.int64)
+    p.gather(src, idx, dst)
+    assert torch.equal(dst, src.index_select(0, idx))
+    with pytest.raises(IndexError):
+        p.gather(src, torch.tensor([97]), dst)
+
+
+def test_native_synthetic_masking_law_and_determinism():
+    cfg = C.get_config("base")
+    ds = NativeSyntheticLM(cfg, 4096, seq_len=128, seed=11)
+    ids, lab = ds.batch(0, 256)
+    assert (ids[:, 0] == 101).all() and (ids[:, -1] == 102).all()
+    masked = lab != IGNORE_INDEX
+    body = torch.ones_like(masked)
+    body[:, 0] = body[:, -1] = False
+    assert not masked[~body].any()                               # special tokens never masked
+    assert abs(masked[body].float().mean().item() - 0.15) < 0.01
+    assert abs((ids[masked] == cfg.mask_token_id).float().mean().item() - 0.8) < 0.02
+    unchanged = (ids[masked] == lab[masked]).float().mean().item()
+    assert abs(unchanged - 0.1) < 0.02                          # 10 % kept (+ rare random hits)
+    assert (lab[masked] >= 104).all()                           # labels are body tokens
+    # a row is a pure function of (seed, row): batch boundaries / thread counts do not matter
+    ids2, lab2 = ds.batch(100, 7)
+    assert torch.equal(ids2, ids[100:107]) and torch.equal(lab2, lab[100:107])
+    ids3, _ = NativeSyntheticLM(cfg, 4096, seq_len=128, seed=12).batch(0, 4)
+    assert not torch.equal(ids3, ids[:4])
+
+
+def test_native_synthetic_causal_rows():
+    cfg = C.get_config("causal-tiny")
+    ids, lab = NativeSyntheticLM(cfg, 16, seq_len=64, seed=3).batch(0, 16)
+    assert torch.equal(ids, lab) and ids.min() >= 0 and ids.max() < cfg.vocab_size
+
+
+def test_loader_with_native_dataset_shards_every_row_once():
+    cfg = C.get_config("bert-tiny")
+    ds = NativeSyntheticLM(cfg, 40, seq_len=32, seed=5)
+    seen = []
+    for rank in range(2):
+        loader = DeviceBatchLoader(ds, 4, sampler=DistributedSampler(ds, 2, rank, shuffle=True), device="cpu")
+        for b in loader:
+            seen.append(b["input_ids"])
+    rows = torch.cat(seen)
+    full, _ = ds.batch(0, 40)
+    assert rows.shape == full.shape
+    key = lambda t: sorted(map(tuple, t.tolist()))  # noqa: E731
+    assert key(rows) == key(full)
