@@ -66,6 +66,9 @@ _SIGS = {
     "dtd_gemm_bt": (I, [I, P, I, P, I, P, I, P, P, I, P, P, I, I, I, P]),
     "dtd_transpose_bf16": (I, [P, P, I, I, P]),
     "dtd_gemm_set_stamps": (I, [P]),
+    "dtd_gemm_tn_supported": (I, [I, I, I]),
+    "dtd_gemm_tn_splits": (I, [I, I, I]),
+    "dtd_gemm_tn": (I, [P, I, P, I, P, I, I, I, I, P]),
     # reduce.hip
     "dtd_splitk_reduce": (I, [P, I, I, ctypes.c_longlong, P, I, I, P]),
 }

@@ -11,6 +11,9 @@ input-gradient product uses the transposed weight, ``transpose``):
 * ``gelu_bwd_gemm(dy, w_t, u, dbias)`` -> du = (dy w_t^T) * gelu'(u) plus the column sums of du
                                       (FFN down-projection dgrad with the GELU derivative and the
                                       up-projection's bias gradient in the epilogue)
+* ``wgrad_tn(dy, x)``              -> fp32 split-K partials of dy^T x (weight gradient of a Linear:
+                                      both operands row-major over the token dim, transposing LDS
+                                      reads; one wave of workgroups; ``grad.splitk_reduce`` sums)
 
 The kernel is the 256x256 8-phase LDS-DMA pipeline of cdna_hip_programming.md §5 (see the .hip
 header).  Shapes must tile by 256 x 256 x 64 (``supported``); callers fall back to hipBLASLt +
@@ -34,6 +37,11 @@ _ENABLED = [os.environ.get("DTD_GEMM", "1") == "1"]
 # the GELU epilogue, and the FFN down-projection dgrad with the GELU-backward epilogue.
 _FFN_FWD = [os.environ.get("DTD_GEMM_FFN_FWD", "1") == "1"]
 _FFN_BWD = [os.environ.get("DTD_GEMM_FFN_BWD", "1") == "1"]
+# TN weight-gradient kernel: off by default -- even on the o-projection, where it wins in
+# isolation, the full-chip split-K grid on the side stream cost 0.35 % end-to-end
+# (profiles/r2_ab_gemm_oproj.jsonl).  The NT kernel on the transposed o-projection weight (152 vs
+# 164 us in isolation) was neutral end-to-end as well and is not wired in.
+_WGRAD = [os.environ.get("DTD_GEMM_WGRAD", "0") == "1"]
 
 
 def enabled() -> bool:
@@ -46,6 +54,10 @@ def ffn_fwd_enabled() -> bool:
 
 def ffn_bwd_enabled() -> bool:
     return _ENABLED[0] and _FFN_BWD[0]
+
+
+def wgrad_enabled() -> bool:
+    return _ENABLED[0] and _WGRAD[0]
 
 
 def set_enabled(on: bool) -> None:
@@ -127,3 +139,30 @@ def transpose(w: torch.Tensor) -> torch.Tensor:
     out = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
     _lib.call("dtd_transpose_bf16", w.data_ptr(), out.data_ptr(), w.shape[0], w.shape[1], _lib.stream())
     return out
+
+
+def wgrad_preferred(o: int, i: int) -> bool:
+    """Where the TN kernel beats hipBLASLt's split-K bmm: small weights (<= 16 output tiles of
+    256 x 256, e.g. the 768 x 768 attention output projection: 165 vs 176 us at 131k tokens).  Its
+    transposing-read main loop runs ~0.85 PF/s, below hipBLASLt on the larger weights
+    (profiles/r2_gemm8_vs_hipblaslt.jsonl), so those stay on the library."""
+    return (o // 256) * (i // 256) <= 16
+
+
+def wgrad_supported(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    """dy [T, o], x [T, i] bf16 row-major views on the GPU with o, i % 256 == 0, T % 64 == 0."""
+    if not (_ok(dy) and _ok(x)) or dy.shape[0] != x.shape[0] or not _lib.has("dtd_gemm_tn"):
+        return False
+    return bool(_lib.lib().dtd_gemm_tn_supported(dy.shape[1], x.shape[1], dy.shape[0]))
+
+
+def wgrad_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+    """fp32 partials [splits, o, i] of dy^T x over contiguous token ranges."""
+    T, o = dy.shape
+    i = x.shape[1]
+    if splits is None:
+        splits = _lib.lib().dtd_gemm_tn_splits(o, i, T)
+    part = torch.empty((splits, o, i), dtype=torch.float32, device=dy.device)
+    _lib.call("dtd_gemm_tn", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), part.data_ptr(), o, i, T,
+              splits, _lib.stream())
+    return part

@@ -179,6 +179,12 @@ def _emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
     dst, acc = grad_dst(p)
     T, o = dy.shape
     i = x.shape[1]
+    if dy.is_cuda and T >= 8192:
+        from . import gemm as G
+        if G.wgrad_enabled() and G.wgrad_preferred(o, i) and G.wgrad_supported(dy, x):
+            # hand-written TN MFMA GEMM: fp32 split-K partials in one wave of workgroups
+            splitk_reduce(G.wgrad_tn(dy, x), dst, acc)
+            return
     s = wgrad_splits(T, o, i) if dy.is_cuda else 1
     if s == 1:
         gemm_into(dst, dy.t(), x, acc)

@@ -94,6 +94,21 @@ def main():
                                lambda: G.gelu_bwd_gemm(x, wt["fc2"], u, dbias=(db, False))),
         "transpose_fc1": (0, lambda: None, lambda: G.transpose(w["fc1"])),
     }
+    # weight gradients: hipBLASLt split-K (16 x T/16-token slices, bf16 partials) + reduce vs the
+    # TN kernel (fp32 partials, one wave of workgroups) + reduce
+    from distributed_training_and_deepspeed_amd.ops.grad import splitk_reduce
+    gw = {n: torch.empty(t.shape, device=dev, dtype=bf) for n, t in w.items()}
+
+    def hip_wgrad(dy_, x_, dst):
+        o_, i_ = dy_.shape[1], x_.shape[1]
+        splitk_reduce(torch.bmm(dy_.view(16, T // 16, o_).transpose(1, 2), x_.view(16, T // 16, i_)), dst, False)
+
+    for n, (dy_, x_) in {"qkv": (dy3, x), "o": (x, x), "fc1": (xf, x), "fc2": (x, xf)}.items():
+        fl = 2 * T * dy_.shape[1] * x_.shape[1]
+        cases[f"wgrad_{n}"] = (fl, lambda dy_=dy_, x_=x_, d=gw[n]: hip_wgrad(dy_, x_, d),
+                               lambda dy_=dy_, x_=x_, d=gw[n]: splitk_reduce(G.wgrad_tn(dy_, x_), d, False))
+    chk["wgrad_fc1"] = rel(G.wgrad_tn(xf[:S], x[:S]).sum(0), xf[:S].float().t() @ x[:S].float())
+    print(json.dumps({"check_wgrad": round(chk["wgrad_fc1"], 6)}), flush=True)
     times = {k: ([], []) for k in cases}
     for k, (_, f0, f1) in cases.items():   # warm-up (TunableOp lookups, code objects)
         f0(), f1()

@@ -94,3 +94,28 @@ def test_gemm_strided_operands_and_many_tiles():
     assert G.supported(M, N, K, a, b)
     c = G.gemm_bt(a, b)
     assert rel(c, a.float() @ b.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("T,o,i,splits", [(64, 256, 256, 1), (4096, 768, 3072, None), (8192, 2304, 768, 5),
+                                          (1024, 512, 256, 64)])
+def test_wgrad_tn_matches_fp32(T, o, i, splits):
+    """dW = dy^T x through the TN kernel's split-K partials (incl. empty splits) + the reduce."""
+    from distributed_training_and_deepspeed_amd.ops.grad import splitk_reduce
+    torch.manual_seed(5)
+    dy = torch.randn(T, o, device="cuda").bfloat16()
+    x = torch.randn(T, i, device="cuda").bfloat16()
+    assert G.wgrad_supported(dy, x)
+    part = G.wgrad_tn(dy, x, splits)
+    ref = dy.float().t() @ x.float()
+    assert rel(part.sum(0), ref) < 2e-3, rel(part.sum(0), ref)
+    dst = torch.full((o, i), 1.0, device="cuda", dtype=torch.float32)
+    splitk_reduce(part, dst, True)
+    assert rel(dst - 1.0, ref) < 2e-3
+
+
+def test_wgrad_tn_asymmetric_detects_transpose():
+    T, n = 256, 256
+    dy = torch.eye(n, device="cuda").bfloat16().repeat(T // n, 1)          # [T, n]
+    x = torch.arange(T * n, device="cuda").float().view(T, n).remainder(13).bfloat16()
+    part = G.wgrad_tn(dy, x, 1)
+    assert torch.equal(part[0], x.float())       # I^T x = x (exact small integers)
