@@ -174,6 +174,70 @@ __global__ void __launch_bounds__(256) attn_mask_kernel(uint32_t* __restrict__ m
   }
 }
 
+// Same masks, fewer VALU issues per decision (the generator is VALU-bound: B*H*S*S decisions).
+//  * A word: d = (thr - 1) - h is negative iff keep, and v_alignbit(word, d, 31) shifts the word
+//    left by one while inserting d's sign bit -- 2 VALU per decision (the 16-bit half selected by
+//    the subtract's SDWA operand) instead of compare + select + or.  Keys enter at bit 0 in
+//    order, so one v_bfrev at the end puts key j at bit j.
+//  * B words: the 32x32 bit matrix held by each 32-lane half (row = query lane, column = key)
+//    is transposed in registers by five block-swap stages (ds_swizzle lane ^ s, v_alignbit
+//    rotate, v_bfi merge): 15 issues per word instead of 64 v_writelane.
+template <int S_>
+__device__ __forceinline__ uint32_t swap_stage(uint32_t t, uint32_t sh, uint32_t mk) {
+  const uint32_t y = (uint32_t)__builtin_amdgcn_ds_swizzle((int)t, (S_ << 10) | 0x1f);   // lane ^ S_ (32-lane groups)
+  const uint32_t rot = __builtin_amdgcn_alignbit(y, y, sh);
+  return (rot & mk) | (t & ~mk);
+}
+__global__ void __launch_bounds__(256) attn_mask_kernel_t(uint32_t* __restrict__ maskA, uint32_t* __restrict__ maskB,
+                                                          int S, int W, const uint64_t* rng, uint32_t sid, uint32_t thr) {
+  DropoutRng g(rng, sid);
+  const int lane = threadIdx.x & 63, bh = blockIdx.y;
+  const int q = blockIdx.x * 64 + lane;
+  const bool qv = q < S;
+  const uint64_t ctr0 = ((uint64_t)bh * S + (uint64_t)(qv ? q : 0)) * (uint64_t)W;
+  // keep <=> h >= thr <=> (thr - 1) - h < 0; lanes past S never keep (h <= 65535)
+  const int thm1 = qv ? (int)thr - 1 : 65535;
+  // per-stage lane constants of the transpose: rotate amount and merge mask
+  uint32_t sh[5], mk[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int s = 16 >> i;
+    const uint32_t Hs = i == 0 ? 0xffff0000u : i == 1 ? 0xff00ff00u : i == 2 ? 0xf0f0f0f0u : i == 3 ? 0xccccccccu : 0xaaaaaaaau;
+    const bool up = lane & s;
+    sh[i] = up ? s : 32 - s;
+    mk[i] = up ? ~Hs : Hs;
+  }
+  const int qw = blockIdx.x * 2 + (lane >> 5);   // query word of the B entry this lane stores
+  for (int kw = threadIdx.x >> 6; kw < W; kw += 4) {
+    uint32_t x = g.bits(ctr0 + kw);
+    x = x ? x : 0x6d2b79f5u;
+    uint32_t word = 0;
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      if (n) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; }
+      word = __builtin_amdgcn_alignbit(word, (uint32_t)(thm1 - (int)(x & 0xffffu)), 31);
+      word = __builtin_amdgcn_alignbit(word, (uint32_t)(thm1 - (int)(x >> 16)), 31);
+    }
+    word = __builtin_bitreverse32(word);
+    const int nk = S - kw * 32;                  // valid keys in this word
+    if (nk < 32) word &= (0xffffffffu >> (32 - nk));
+    if (qv) maskA[((size_t)bh * W + kw) * S + q] = word;
+    uint32_t t = word;
+    t = swap_stage<16>(t, sh[0], mk[0]);
+    t = swap_stage<8>(t, sh[1], mk[1]);
+    t = swap_stage<4>(t, sh[2], mk[2]);
+    t = swap_stage<2>(t, sh[3], mk[3]);
+    t = swap_stage<1>(t, sh[4], mk[4]);
+    const int key = kw * 32 + (lane & 31);
+    if (key < S && qw < W) maskB[((size_t)bh * W + qw) * S + key] = t;
+  }
+}
+
+static bool mask_ballot() {
+  static const int v = [] { const char* e = getenv("DTD_ATTN_MASK"); return e && e[0] == '0' ? 1 : 0; }();
+  return v != 0;
+}
+
 // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs, each with its own
 // L2; in HW order the gridDim.x tiles of one (batch, head) -- which all stream the same K/V
 // (dK/dV: Q/dO) -- would land on gridDim.x different XCDs and fetch those operands once per XCD.
@@ -813,8 +877,8 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
     // stream, overlapping the QKV GEMM)
     if (rng) {
       uint32_t* mB = masks + (size_t)B * H * S * W;
-      hipLaunchKernelGGL(attn_mask_kernel, dim3((S + 63) / 64, B * H), dim3(256), 0, s, mA, mB, S, W, rng, sid,
-                         keep_threshold(p));
+      hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : attn_mask_kernel_t, dim3((S + 63) / 64, B * H), dim3(256), 0,
+                         s, mA, mB, S, W, rng, sid, keep_threshold(p));
     }
   }
   const char* thr_env = getenv("DTD_ATTN_RESCALE_THR");
@@ -842,8 +906,8 @@ DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, con
   if (B * S * H == 0 || p <= 0.f) return 0;
   if (!masks || !rng) return (int)hipErrorInvalidValue;
   const int W = (S + 31) / 32;
-  hipLaunchKernelGGL(attn_mask_kernel, dim3((S + 63) / 64, B * H), dim3(256), 0, s, masks, masks + (size_t)B * H * S * W,
-                     S, W, rng, sid, keep_threshold(p));
+  hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : attn_mask_kernel_t, dim3((S + 63) / 64, B * H), dim3(256), 0, s,
+                     masks, masks + (size_t)B * H * S * W, S, W, rng, sid, keep_threshold(p));
   DTD_LAUNCH_CHECK();
 }
 
