@@ -77,8 +77,15 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 // Dropout as a bit select: all-ones / zero lane mask from bit `b` of `w` (one v_bfe_i32), AND-ed
 // into the float's bits -- 2 VALU per element instead of shift/compare/select/multiply; the
 // 1/(1-p) rescale is folded into the per-row epilogue.
+// The empty asm hides that the mask is 0 / -1: otherwise the compiler rewrites the AND into
+// v_and (bit test) + v_cmp + v_cndmask, with an s_nop for the VCC hazard -- 3-4 issues a score.
+__device__ __forceinline__ int bit_mask(uint32_t w, int b) {
+  int m = __builtin_amdgcn_sbfe((int)w, b, 1);
+  asm("" : "+v"(m));
+  return m;
+}
 __device__ __forceinline__ float keep_bits(float v, uint32_t w, int b) {
-  return __int_as_float(__float_as_int(v) & __builtin_amdgcn_sbfe((int)w, b, 1));
+  return __int_as_float(__float_as_int(v) & bit_mask(w, b));
 }
 
 // Lane l <-> lane l^32 combine with v_permlane32_swap (a VALU op; __shfl_xor(x, 32) would be a
@@ -251,25 +258,64 @@ __device__ __forceinline__ void xcd_tile(int& tx, int& ty) {
   ty = T / nx;
 }
 
-// Stage a [rows x D] bf16 tile (row stride `ld` in global) into registers, then LDS.
+// Bounded buffer resource (base readfirstlane'd into SGPRs): loads at byte offsets >= `bytes`
+// return 0 without touching memory, which is how the tile loads below handle rows past S and
+// absent dropout masks (bytes = 0) with no per-lane clamp or select.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bounded_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)bytes, 0x00020000);
+}
+
+// The [nrows x D] bf16 rows (row stride ld elements) of one (batch, head): a bounded resource,
+// this thread's byte offset inside a tile, and the row pitch.  A tile load is then one
+// buffer_load_dwordx4 per chunk with the row offset in an SGPR -- no per-tile VALU address math
+// (64-bit multiply-adds, clamps and zeroing selects cost ~40 VALU a tile in the VALU-bound loops).
+struct RowSrc {
+  __amdgpu_buffer_rsrc_t rs;
+  int voff, ld2;
+};
+template <int D>
+__device__ __forceinline__ RowSrc row_src(const bf16* base, int ld, int nrows) {
+  RowSrc r;
+  r.rs = bounded_rsrc(base, nrows > 0 ? (uint32_t)(((nrows - 1) * ld + D) * 2) : 0u);
+  r.voff = ((threadIdx.x / (D / 8)) * ld + (threadIdx.x % (D / 8)) * 8) * 2;
+  r.ld2 = ld * 2;
+  return r;
+}
+// One dropout keep word per lane (its query / key `pos`) per 32-wide word index: [W][S] uint32
+// words of one (batch, head); indices past W (and every index when there is no mask) read 0.
+struct WordSrc {
+  __amdgpu_buffer_rsrc_t rs;
+  int voff, stride;
+  __device__ __forceinline__ uint32_t load(int wi) const {
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, voff, wi * stride, 0);
+  }
+};
+__device__ __forceinline__ WordSrc word_src(const uint32_t* words, const void* dummy, int W, int S, int pos) {
+  WordSrc w;
+  w.rs = bounded_rsrc(words ? (const void*)words : dummy, words ? (uint32_t)W * S * 4u : 0u);
+  w.voff = pos * 4;
+  w.stride = S * 4;
+  return w;
+}
+
+// Stage a [rows x D] bf16 tile into registers, then LDS.
 template <int D, int ROWS>
 struct TileLoader {
   static constexpr int CH = ROWS * D / 8;  // 16-byte chunks
   static constexpr int PER = (CH + 255) / 256;
+  static constexpr int RPI = 256 / (D / 8);  // rows per 256-chunk round
   bf16x8 reg[PER];
   static_assert(CH % 256 == 0, "tile must split evenly over 256 threads");
-  // Branch-free: rows past the end are loaded from the last valid row and zeroed by a select, so
-  // the loads form straight-line code and the compiler can count them (partial vmcnt waits)
-  // while a second tile's loads are still in flight (the register ring of the kernels below).
-  __device__ __forceinline__ void load(const bf16* base, int ld, int row0, int nrows) {
+  // straight-line loads (rows past the end read 0 through the bounded resource), so the
+  // compiler can count them (partial vmcnt waits) while a second tile's loads are in flight
+  // (the register ring of the kernels below)
+  __device__ __forceinline__ void load(const RowSrc& src, int row0) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      const int rr = c / (D / 8), dc = (c % (D / 8)) * 8;
-      const int row = min(row0 + rr, nrows - 1);
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(base + (size_t)row * ld + dc);
-      reg[i] = (row0 + rr < nrows) ? v : bf16x8{};
-    }
+    for (int i = 0; i < PER; ++i)
+      reg[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(src.rs, src.voff, (row0 + RPI * i) * src.ld2, 0));
   }
   __device__ __forceinline__ void store(bf16* lds, int stride) const {
 #pragma unroll
@@ -304,9 +350,9 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   const float sc2 = a.scale * kLog2e;
   const bool drop = a.maskA != nullptr;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
-  const uint32_t* mcol = drop ? a.maskA + (size_t)bh * a.W * S + (qvalid ? q : 0) : nullptr;
-  const bf16* kbase = a.k + (size_t)b * S * a.ld + h * D;
-  const bf16* vbase = a.v + (size_t)b * S * a.ld + h * D;
+  const RowSrc ksrc = row_src<D>(a.k + (size_t)b * S * a.ld + h * D, a.ld, S);
+  const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
+  const WordSrc wsrc = word_src(drop ? a.maskA + (size_t)bh * a.W * S : nullptr, a.lse, a.W, S, qvalid ? q : 0);
 
   bf16x8 qf[NC];
   {
@@ -332,25 +378,20 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   TileLoader<D, BN>& vl1 = RING == 2 ? vl1r : vl0;
   uint32_t mwc[NKB], mw0[NKB], mw1r[NKB];
   uint32_t* mw1 = RING == 2 ? mw1r : mw0;
-  // unconditional word loads (a valid dummy address without dropout) keep the ring branch-free
-  const uint32_t* wbase = drop ? mcol : reinterpret_cast<const uint32_t*>(a.lse);
-  const size_t wstride = drop ? (size_t)S : 0;
+  // unconditional word loads (zeros without dropout) keep the ring branch-free
   auto load_words = [&](int k0, uint32_t* out) {
 #pragma unroll
-    for (int j = 0; j < NKB; ++j) {
-      const int kw = min((k0 >> 5) + j, a.W - 1);
-      out[j] = wbase[(size_t)kw * wstride];
-    }
+    for (int j = 0; j < NKB; ++j) out[j] = wsrc.load((k0 >> 5) + j);
   };
   load_words(0, mwc);
-  kl0.load(kbase, a.ld, 0, S);
-  vl0.load(vbase, a.ld, 0, S);
+  kl0.load(ksrc, 0);
+  vl0.load(vsrc, 0);
   kl0.store(Ks[0], KP);
   vl0.store(Vs[0], VP);
   {
     const int k1 = min(1, nt - 1) * BN, k2 = min(2, nt - 1) * BN;
-    kl1.load(kbase, a.ld, k1, S); vl1.load(vbase, a.ld, k1, S); load_words(k1, mw1);
-    if constexpr (RING == 2) { kl0.load(kbase, a.ld, k2, S); vl0.load(vbase, a.ld, k2, S); load_words(k2, mw0); }
+    kl1.load(ksrc, k1); vl1.load(vsrc, k1); load_words(k1, mw1);
+    if constexpr (RING == 2) { kl0.load(ksrc, k2); vl0.load(vsrc, k2); load_words(k2, mw0); }
   }
   __syncthreads();
   // SET = register set holding tile t+1 (t even -> 1, t odd -> 0)
@@ -411,13 +452,13 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     const float msc = slow ? 1.f : sc2;
     // l stays a per-half partial (both halves share m, hence every rescale); the two halves
     // are combined once in the epilogue.  Four independent partial sums shorten the add chain.
-    float ps[4] = {0.f, 0.f, 0.f, 0.f};
+    float ps[4];
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float pv = fexp2(fmaf(sacc[kb][i], msc, -mexp));
-        ps[i & 3] += pv;
+        ps[i & 3] = (kb == 0 && i < 4) ? pv : ps[i & 3] + pv;   // no "+ 0" adds (-0 semantics keep them)
         sacc[kb][i] = pv;
       }
     l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
@@ -447,8 +488,8 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
       for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
       // tile t+1+RING (clamped to the last tile: a harmless reload keeps the issue unconditional)
       const int kf = min(t + 1 + RING, nt - 1) * BN;
-      kn.load(kbase, a.ld, kf, S);
-      vn.load(vbase, a.ld, kf, S);
+      kn.load(ksrc, kf);
+      vn.load(vsrc, kf);
       load_words(kf, mwn);
     }
     __syncthreads();
@@ -506,9 +547,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   constexpr bool drop = DROP;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
   const float kbias = sl2 * (float)key;   // ALiBi bias of this lane's key (0 without ALiBi)
-  const uint32_t* mcol = drop ? a.maskB + (size_t)bh * a.W * S + (kvalid ? key : 0) : nullptr;
-  const bf16* qbase = a.q + (size_t)b * S * a.ld + h * D;
-  const bf16* obase = a.dout + (size_t)b * S * a.ldo + h * D;
+  const WordSrc wsrc = word_src(drop ? a.maskB + (size_t)bh * a.W * S : nullptr, a.lse, a.W, S, kvalid ? key : 0);
+  const RowSrc qsrc = row_src<D>(a.q + (size_t)b * S * a.ld + h * D, a.ld, S);
+  const RowSrc osrc = row_src<D>(a.dout + (size_t)b * S * a.ldo + h * D, a.ldo, S);
   const float* lseb = a.lse + (size_t)bh * S;
   const float* delb = a.delta + (size_t)bh * S;
 
@@ -544,11 +585,11 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < NQW; ++j) {
       const int qw = (q0 >> 5) + j;
-      out[j] = drop && qw < a.W ? mcol[(size_t)qw * S] : 0u;
+      out[j] = drop ? wsrc.load(qw) : 0u;
     }
   };
-  ql.load(qbase, a.ld, qstart, S);
-  ol.load(obase, a.ldo, qstart, S);
+  ql.load(qsrc, qstart);
+  ol.load(osrc, qstart);
   load_stats(qstart);
   load_words(qstart, mwc);
   ql.store(Qs[0], QP);
@@ -558,8 +599,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   for (int t = 0; t < nt; ++t) {
     const int buf = t & 1, q0 = qstart + t * BM;
     if (t + 1 < nt) {
-      ql.load(qbase, a.ld, q0 + BM, S);
-      ol.load(obase, a.ldo, q0 + BM, S);
+      ql.load(qsrc, q0 + BM);
+      ol.load(osrc, q0 + BM);
       load_stats(q0 + BM);
       load_words(q0 + BM, mwn);
     }
@@ -614,8 +655,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       for (int i = 0; i < 16; i += 2) {
         const f32x2 nd = pk2(D4[i >> 2][i & 3], D4[i >> 2][(i & 3) + 1]);
         if constexpr (DROP) {
-          const int m0 = __builtin_amdgcn_sbfe((int)mw, crow(i, 0), 1);
-          const int m1 = __builtin_amdgcn_sbfe((int)mw, crow(i + 1, 0), 1);
+          const int m0 = bit_mask(mw, crow(i, 0));
+          const int m1 = bit_mask(mw, crow(i + 1, 0));
           const f32x2 t = pk_fma(pk2(mask_bits(pacc[i], m0), mask_bits(pacc[i + 1], m1)), pk2(inv_keep, inv_keep), nd);
           const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * t;                 // dS
           pacc[i] = ds.x;
@@ -686,9 +727,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   const float sc2 = a.scale * kLog2e;
   const bool drop = a.maskA != nullptr;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
-  const uint32_t* mcol = drop ? a.maskA + (size_t)bh * a.W * S + (qvalid ? q : 0) : nullptr;
-  const bf16* kbase = a.k + (size_t)b * S * a.ld + h * D;
-  const bf16* vbase = a.v + (size_t)b * S * a.ld + h * D;
+  const RowSrc ksrc = row_src<D>(a.k + (size_t)b * S * a.ld + h * D, a.ld, S);
+  const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
+  const WordSrc wsrc = word_src(drop ? a.maskA + (size_t)bh * a.W * S : nullptr, a.lse, a.W, S, qvalid ? q : 0);
 
   bf16x8 qf[NC], of[NC];
   {
@@ -731,25 +772,20 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   TileLoader<D, BN>& vl1 = RING == 2 ? vl1r : vl0;
   uint32_t mwc[NKB], mw0[NKB], mw1r[NKB];
   uint32_t* mw1 = RING == 2 ? mw1r : mw0;
-  // unconditional word loads (a valid dummy address without dropout) keep the ring branch-free
-  const uint32_t* wbase = drop ? mcol : reinterpret_cast<const uint32_t*>(a.lse);
-  const size_t wstride = drop ? (size_t)S : 0;
+  // unconditional word loads (zeros without dropout) keep the ring branch-free
   auto load_words = [&](int k0, uint32_t* out) {
 #pragma unroll
-    for (int j = 0; j < NKB; ++j) {
-      const int kw = min((k0 >> 5) + j, a.W - 1);
-      out[j] = wbase[(size_t)kw * wstride];
-    }
+    for (int j = 0; j < NKB; ++j) out[j] = wsrc.load((k0 >> 5) + j);
   };
   load_words(0, mwc);
-  kl0.load(kbase, a.ld, 0, S);
-  vl0.load(vbase, a.ld, 0, S);
+  kl0.load(ksrc, 0);
+  vl0.load(vsrc, 0);
   kl0.store(Ks[0], KP);
   vl0.store(Vs[0], KP);
   {
     const int k1 = min(1, nt - 1) * BN, k2 = min(2, nt - 1) * BN;
-    kl1.load(kbase, a.ld, k1, S); vl1.load(vbase, a.ld, k1, S); load_words(k1, mw1);
-    if constexpr (RING == 2) { kl0.load(kbase, a.ld, k2, S); vl0.load(vbase, a.ld, k2, S); load_words(k2, mw0); }
+    kl1.load(ksrc, k1); vl1.load(vsrc, k1); load_words(k1, mw1);
+    if constexpr (RING == 2) { kl0.load(ksrc, k2); vl0.load(vsrc, k2); load_words(k2, mw0); }
   }
   __syncthreads();
   auto tile = [&](auto set_c, int t) {
@@ -807,8 +843,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
       for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
       // tile t+1+RING (clamped to the last tile: a harmless reload keeps the issue unconditional)
       const int kf = min(t + 1 + RING, nt - 1) * BN;
-      kn.load(kbase, a.ld, kf, S);
-      vn.load(vbase, a.ld, kf, S);
+      kn.load(ksrc, kf);
+      vn.load(vsrc, kf);
       load_words(kf, mwn);
     }
     __syncthreads();
@@ -864,10 +900,17 @@ static int tile_keys(int which) {
 
 // q,k,v,o: bf16 views with row stride ld (q/k/v) / ldo (o); lse: [B,H,S] fp32.
 // masks: [2][B*H*S*W] uint32 (W = ceil(S/32)) written here when p > 0 (read by the backward).
+// The tile loads address one (batch, head)'s rows through 32-bit buffer offsets (RowSrc).
+static bool offsets_fit(int S, int ld, int ldo) {
+  const long long lim = 0x7fffffffLL;
+  return (long long)S * ld * 2 < lim && (long long)S * ldo * 2 < lim && (long long)S * ((S + 31) / 32) * 4 < lim;
+}
+
 DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const float* slopes,
                             uint32_t* masks, int B, int S, int H, int D, int ld, int ldo, int causal, float scale,
                             float p, const uint64_t* rng, uint32_t sid, hipStream_t s) {
   if (B * S * H == 0) return 0;
+  if (!offsets_fit(S, ld, ldo)) return (int)hipErrorInvalidValue;
   const int W = (S + 31) / 32;
   uint32_t* mA = nullptr;
   if (p > 0.f) {
@@ -927,6 +970,7 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
                             float p, hipStream_t s) {
   if (B * S * H == 0) return 0;
   if (D != 64 && D != 128) return (int)hipErrorInvalidValue;
+  if (!offsets_fit(S, ld, ldo)) return (int)hipErrorInvalidValue;
   const int W = (S + 31) / 32;
   const uint32_t* mA = (p > 0.f) ? masks : nullptr;
   const uint32_t* mB = (p > 0.f) ? masks + (size_t)B * H * S * W : nullptr;
