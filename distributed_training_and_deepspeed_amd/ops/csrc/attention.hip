@@ -530,9 +530,18 @@ struct BwdArgs {
 template <int D, int OCC, int BM, bool DROP, bool ALIBI>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   constexpr int QP = D + 8, NC = D / 16, NDB = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * QP];
-  __shared__ __attribute__((aligned(16))) bf16 Os[2][BM * QP];
-  __shared__ __attribute__((aligned(16))) float lse_s[2][BM], del_s[2][BM];
+  // One LDS block, row statistics first: placed after the 72 KiB of Q/dO tiles (BM = 128) their
+  // ds_read offsets exceed the 16-bit immediate and every read needed a VALU address add.
+  struct Smem {
+    float lse_s[2][BM], del_s[2][BM];
+    bf16 Qs[2][BM * QP];
+    bf16 Os[2][BM * QP];
+  };
+  __shared__ __attribute__((aligned(16))) Smem sm;
+  auto& lse_s = sm.lse_s;
+  auto& del_s = sm.del_s;
+  auto& Qs = sm.Qs;
+  auto& Os = sm.Os;
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, r = lane & 31;
   int tx, ty;

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# attention: dropout keep masks as scalar-loaded lane masks (v_cndmask with SGPR pair): tests, kernel times, bench A/B.
+# attention dK/dV: single LDS block with row statistics first (immediate ds_read offsets): tests, kernel times, bench A/B.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 source scripts/gpu_step.sh
 export TMPDIR=/tmp
