@@ -203,8 +203,9 @@ def _acc(p):
 
 def _ffn_gemm_ok(c, x: torch.Tensor, w: torch.Tensor, *more) -> bool:
     """The hand-written GEMM with the GELU epilogues (ops/csrc/gemm.hip) takes the FFN products
-    when the activation is GELU(erf), the tensors are bf16 on the GPU and the shape tiles by 256."""
-    return (c.activation == "gelu" and x.is_cuda and x.dtype == torch.bfloat16 and G.enabled()
+    when the activation is GELU (erf or tanh), the tensors are bf16 on the GPU and the shape tiles
+    by 256."""
+    return (c.activation in G.FUSED_ACTS and x.is_cuda and x.dtype == torch.bfloat16 and G.enabled()
             and G.supported(x.shape[0], w.shape[0], x.shape[1], x, w, *more))
 
 
@@ -243,7 +244,7 @@ class _FusedLayerFn(torch.autograd.Function):
         else:
             z1, f_in, m1, r1 = Fx.ln_fwd(o, x2d, g1, b1, eps, p_h, rng, s1)
         if G.ffn_fwd_enabled() and _ffn_gemm_ok(c, f_in, w1):
-            u, a = G.linear_gelu(f_in, w1, bf1)     # fc1 + bias + GELU in one kernel
+            u, a = G.linear_gelu(f_in, w1, bf1, c.activation)     # fc1 + bias + GELU in one kernel
         else:
             u = F.linear(f_in, w1, bf1)
             a = Fx.act_fwd(u, c.activation)
@@ -288,12 +289,12 @@ class _FusedLayerFn(torch.autograd.Function):
         # dgrad first; without a kept forward activation, a = act(u) (fc2's wgrad input) is
         # recomputed inside the activation-backward pass (no separate act_fwd read/write)
         w2t = None
-        if (a is not None and G.ffn_bwd_enabled() and c.activation == "gelu" and dy.is_cuda
+        if (a is not None and G.ffn_bwd_enabled() and c.activation in G.FUSED_ACTS and dy.is_cuda
                 and dy.dtype == torch.bfloat16 and G.supported(dy.shape[0], w2.shape[1], dy.shape[1], dy, u)):
             w2t = G.transpose(w2)                      # [ffn, hidden]: K-contiguous B operand
         if w2t is not None:
             # fc2 dgrad, GELU' and fc1's bias gradient in one kernel (no da round trip)
-            du = G.gelu_bwd_gemm(dy, w2t, u, dbias=_acc(bf1))
+            du = G.gelu_bwd_gemm(dy, w2t, u, dbias=_acc(bf1), act=c.activation)
             del w2t
         else:
             da = dy @ w2

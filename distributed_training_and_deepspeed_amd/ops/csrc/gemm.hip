@@ -10,6 +10,8 @@
 //   EPI_GELU_BWD   dU = bf16(acc) * gelu'(U); store dU; column   FFN down-projection dgrad + GELU'
 //                  partial sums of dU (the up-projection's bias gradient, finalised by colsum)
 //   EPI_ADD        C = C + acc (in place)                       residual-branch dgrad (post-LN BERT)
+//   EPI_BIAS_GELU_TANH / EPI_GELU_TANH_BWD: the same two GELU epilogues with the tanh
+//                  approximation (GPT-2 / BLOOM "gelu_new")
 //
 // Main loop (cdna_hip_programming.md §5, "256² 8-phase template"): 256x256 output tile per
 // 512-thread workgroup, 8 waves as 2 (M) x 4 (N), each wave 128 x 64 as 8 x 4 tiles of
@@ -45,7 +47,10 @@ constexpr int A_BYTES = BM * BK * 2;             // 32 KiB
 constexpr int TILE_BYTES = (BM + BN) * BK * 2;   // 64 KiB per K-step buffer
 constexpr int LDS_BYTES = 2 * TILE_BYTES;        // 128 KiB
 
-enum Epi : int { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_GELU_BWD = 2, EPI_ADD = 3 };
+enum Epi : int { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_GELU_BWD = 2, EPI_ADD = 3, EPI_BIAS_GELU_TANH = 4,
+                 EPI_GELU_TANH_BWD = 5 };
+__host__ __device__ constexpr bool is_gelu_fwd(int e) { return e == EPI_BIAS_GELU || e == EPI_BIAS_GELU_TANH; }
+__host__ __device__ constexpr bool is_gelu_bwd(int e) { return e == EPI_GELU_BWD || e == EPI_GELU_TANH_BWD; }
 
 struct GemmArgs {
   const bf16* a; const bf16* b;          // A [M, K] (lda), B [N, K] (ldb)
@@ -99,6 +104,30 @@ __device__ __forceinline__ float phi_cdf(float x, float e) {
   return 0.5f + 0.5f * copysignf(1.f - poly * e, x);
 }
 __device__ __forceinline__ float gelu(float x) { return x * phi_cdf(x, __expf(-0.5f * x * x)); }
+// tanh GELU: 0.5 x (1 + tanh(k (x + 0.044715 x^3))), tanh from one v_exp + one v_rcp (saturates
+// correctly at +-inf) -- the same formula as ops/csrc/act.hip
+__device__ __forceinline__ float tanh_fast(float y) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * y)); }
+__device__ __forceinline__ float gelu_tanh(float x) {
+  return 0.5f * x * (1.f + tanh_fast(0.7978845608028654f * fmaf(0.044715f * x, x * x, x)));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k = 0.7978845608028654f;
+  const float t = tanh_fast(k * fmaf(0.044715f * x, x * x, x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+}
+template <int EPI> __device__ __forceinline__ float epi_act(float x);
+template <int EPI> __device__ __forceinline__ float epi_act_grad(float x);
+__device__ __forceinline__ float gelu_grad(float x);
+template <int EPI>
+__device__ __forceinline__ float epi_act(float x) {
+  if constexpr (EPI == EPI_BIAS_GELU_TANH) return gelu_tanh(x);
+  else return gelu(x);
+}
+template <int EPI>
+__device__ __forceinline__ float epi_act_grad(float x) {
+  if constexpr (EPI == EPI_GELU_TANH_BWD) return gelu_tanh_grad(x);
+  else return gelu_grad(x);
+}
 __device__ __forceinline__ float gelu_grad(float x) {
   const float e = __expf(-0.5f * x * x);
   return fmaf(x * 0.3989422804014327f, e, phi_cdf(x, e));
@@ -273,7 +302,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_kernel(GemmArgs g) {
   for (int ni = 0; ni < 4; ++ni) {
     const int n = wn * 64 + ni * 16 + 4 * lq;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI == EPI_STORE || EPI == EPI_BIAS_GELU) {
+    if constexpr (EPI == EPI_STORE || is_gelu_fwd(EPI)) {
       if (g.bias) {
         const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n0 + n);
 #pragma unroll
@@ -316,10 +345,10 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_kernel(GemmArgs g) {
     const size_t off = (size_t)(m0 + r) * g.ldc + n0 + c * 8;
     if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
       *reinterpret_cast<bf16x8*>(g.c + off) = v;
-    } else if constexpr (EPI == EPI_BIAS_GELU) {
+    } else if constexpr (is_gelu_fwd(EPI)) {
       bf16x8 a;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = (bf16)gelu((float)v[j]);   // GELU of the stored (bf16) U
+      for (int j = 0; j < 8; ++j) a[j] = (bf16)epi_act<EPI>((float)v[j]);   // GELU of the stored (bf16) U
       *reinterpret_cast<bf16x8*>(g.c + off) = v;
       *reinterpret_cast<bf16x8*>(g.c2 + off) = a;
     } else {   // EPI_GELU_BWD: v = bf16(dA)
@@ -327,7 +356,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_kernel(GemmArgs g) {
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float du = (float)v[j] * gelu_grad((float)u8[j]);
+        const float du = (float)v[j] * epi_act_grad<EPI>((float)u8[j]);
         o[j] = (bf16)du;
         colsum[j] += du;
       }
@@ -339,7 +368,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_kernel(GemmArgs g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   STAMP(5, 0);
 #endif
-  if constexpr (EPI == EPI_GELU_BWD) {
+  if constexpr (is_gelu_bwd(EPI)) {
     if (!g.part) return;
     // lanes c and c+32 hold the same columns; then the 8 waves combine through LDS
 #pragma unroll
@@ -541,7 +570,7 @@ __global__ void __launch_bounds__(512, 2) gemm_tn_kernel(TnArgs g) {
 // vector-memory instructions every wave issues in one epilogue (loads + stores): the lower
 // bound of what sits between a K-step-0 DMA and the next tile's first waits
 constexpr int kStores(int epi) {
-  return epi == EPI_BIAS_GELU ? 32 : epi == EPI_GELU_BWD ? 32 : epi == EPI_ADD ? 48 : 16;
+  return is_gelu_fwd(epi) ? 32 : is_gelu_bwd(epi) ? 32 : epi == EPI_ADD ? 48 : 16;
 }
 
 __device__ __forceinline__ void tile_of(int t, int ntn, int& m0, int& n0) {
@@ -696,7 +725,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (EPI == EPI_STORE || EPI == EPI_BIAS_GELU) {
+        if constexpr (EPI == EPI_STORE || is_gelu_fwd(EPI)) {
           if (g.bias) {
             const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n0 + wn * 64 + ni * 16 + 4 * lq);
 #pragma unroll
@@ -715,7 +744,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
     const int c = lane & 31;
     // row-phase inputs first (GELU_BWD: U), so no later load wait holds back a store
     bf16x8 uin[2][8];
-    if constexpr (EPI == EPI_GELU_BWD) {
+    if constexpr (is_gelu_bwd(EPI)) {
       const auto rs = uniform_rsrc(g.u + (size_t)m0 * g.ldu + n0);
       const int voff = ((w * 16 + (lane >> 5)) * g.ldu + c * 8) * 2;
 #pragma unroll
@@ -751,17 +780,17 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
         const size_t off = (size_t)(m0 + rr * 128 + r) * g.ldc + n0 + c * 8;
         if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
           *reinterpret_cast<bf16x8*>(g.c + off) = v;
-        } else if constexpr (EPI == EPI_BIAS_GELU) {
+        } else if constexpr (is_gelu_fwd(EPI)) {
           bf16x8 av;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) av[j] = (bf16)gelu((float)v[j]);
+          for (int j = 0; j < 8; ++j) av[j] = (bf16)epi_act<EPI>((float)v[j]);
           *reinterpret_cast<bf16x8*>(g.c + off) = v;
           *reinterpret_cast<bf16x8*>(g.c2 + off) = av;
         } else {
           bf16x8 o;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float du = (float)v[j] * gelu_grad((float)uin[rr][i][j]);
+            const float du = (float)v[j] * epi_act_grad<EPI>((float)uin[rr][i][j]);
             o[j] = (bf16)du;
             colsum[j] += du;
           }
@@ -770,7 +799,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
       }
       bar();   // the image is consumed before it is rewritten / restaged
     }
-    if constexpr (EPI == EPI_GELU_BWD) {
+    if constexpr (is_gelu_bwd(EPI)) {
       // lanes c and c+32 hold the same columns; the 8 waves combine through LDS: one fp32
       // partial row per 256-row tile
 #pragma unroll
@@ -893,8 +922,9 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
   if (!dtd_gemm_bt_supported(M, N, K)) return (int)hipErrorInvalidValue;
   if ((lda | ldb | ldc) % 8 || (u && ldu % 8)) return (int)hipErrorInvalidValue;
   if (lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
-  if (epi == EPI_BIAS_GELU && !c2) return (int)hipErrorInvalidValue;
-  if (epi == EPI_GELU_BWD && !u) return (int)hipErrorInvalidValue;
+  if (epi < EPI_STORE || epi > EPI_GELU_TANH_BWD) return (int)hipErrorInvalidValue;
+  if (is_gelu_fwd(epi) && !c2) return (int)hipErrorInvalidValue;
+  if (is_gelu_bwd(epi) && !u) return (int)hipErrorInvalidValue;
   GemmArgs g{(const bf16*)a, (const bf16*)b, (bf16*)c, (bf16*)c2, (const bf16*)u, (const bf16*)bias, part,
              M, N, K, lda, ldb, ldc, ldu, g_stamps};
   const int ntiles = (M / BM) * (N / BN);
@@ -907,6 +937,8 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
       case EPI_BIAS_GELU: DTD_GEMM_P(EPI_BIAS_GELU); break;
       case EPI_GELU_BWD: DTD_GEMM_P(EPI_GELU_BWD); break;
       case EPI_ADD: DTD_GEMM_P(EPI_ADD); break;
+      case EPI_BIAS_GELU_TANH: DTD_GEMM_P(EPI_BIAS_GELU_TANH); break;
+      case EPI_GELU_TANH_BWD: DTD_GEMM_P(EPI_GELU_TANH_BWD); break;
       default: return (int)hipErrorInvalidValue;
     }
 #undef DTD_GEMM_P
@@ -918,6 +950,8 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
     case EPI_BIAS_GELU: hipLaunchKernelGGL(gemm_bt_kernel<EPI_BIAS_GELU>, grid, dim3(512), 0, s, g); break;
     case EPI_GELU_BWD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_GELU_BWD>, grid, dim3(512), 0, s, g); break;
     case EPI_ADD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_ADD>, grid, dim3(512), 0, s, g); break;
+    case EPI_BIAS_GELU_TANH: hipLaunchKernelGGL(gemm_bt_kernel<EPI_BIAS_GELU_TANH>, grid, dim3(512), 0, s, g); break;
+    case EPI_GELU_TANH_BWD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_GELU_TANH_BWD>, grid, dim3(512), 0, s, g); break;
     default: return (int)hipErrorInvalidValue;
   }
   DTD_LAUNCH_CHECK();
