@@ -10,8 +10,8 @@
 //   EPI_GELU_BWD   dU = bf16(acc) * gelu'(U); store dU; column   FFN down-projection dgrad + GELU'
 //                  partial sums of dU (the up-projection's bias gradient, finalised by colsum)
 //   EPI_ADD        C = C + acc (in place)                       residual-branch dgrad (post-LN BERT)
-//   EPI_BIAS_GELU_TANH / EPI_GELU_TANH_BWD: the same two GELU epilogues with the tanh
-//                  approximation (GPT-2 / BLOOM "gelu_new")
+//   EPI_BIAS_GELU_TANH / EPI_GELU_TANH_BWD, EPI_BIAS_RELU / EPI_RELU_BWD: the same two
+//                  activation epilogues for tanh GELU (GPT-2 / BLOOM "gelu_new") and ReLU (OPT)
 //
 // Main loop (cdna_hip_programming.md §5, "256² 8-phase template"): 256x256 output tile per
 // 512-thread workgroup, 8 waves as 2 (M) x 4 (N), each wave 128 x 64 as 8 x 4 tiles of
@@ -48,9 +48,14 @@ constexpr int TILE_BYTES = (BM + BN) * BK * 2;   // 64 KiB per K-step buffer
 constexpr int LDS_BYTES = 2 * TILE_BYTES;        // 128 KiB
 
 enum Epi : int { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_GELU_BWD = 2, EPI_ADD = 3, EPI_BIAS_GELU_TANH = 4,
-                 EPI_GELU_TANH_BWD = 5 };
-__host__ __device__ constexpr bool is_gelu_fwd(int e) { return e == EPI_BIAS_GELU || e == EPI_BIAS_GELU_TANH; }
-__host__ __device__ constexpr bool is_gelu_bwd(int e) { return e == EPI_GELU_BWD || e == EPI_GELU_TANH_BWD; }
+                 EPI_GELU_TANH_BWD = 5, EPI_BIAS_RELU = 6, EPI_RELU_BWD = 7 };
+// activation epilogues (the names keep "gelu" for the family: store U and act(U) / act'(U) . dA)
+__host__ __device__ constexpr bool is_gelu_fwd(int e) {
+  return e == EPI_BIAS_GELU || e == EPI_BIAS_GELU_TANH || e == EPI_BIAS_RELU;
+}
+__host__ __device__ constexpr bool is_gelu_bwd(int e) {
+  return e == EPI_GELU_BWD || e == EPI_GELU_TANH_BWD || e == EPI_RELU_BWD;
+}
 
 struct GemmArgs {
   const bf16* a; const bf16* b;          // A [M, K] (lda), B [N, K] (ldb)
@@ -121,11 +126,13 @@ __device__ __forceinline__ float gelu_grad(float x);
 template <int EPI>
 __device__ __forceinline__ float epi_act(float x) {
   if constexpr (EPI == EPI_BIAS_GELU_TANH) return gelu_tanh(x);
+  else if constexpr (EPI == EPI_BIAS_RELU) return x > 0.f ? x : 0.f;
   else return gelu(x);
 }
 template <int EPI>
 __device__ __forceinline__ float epi_act_grad(float x) {
   if constexpr (EPI == EPI_GELU_TANH_BWD) return gelu_tanh_grad(x);
+  else if constexpr (EPI == EPI_RELU_BWD) return x > 0.f ? 1.f : 0.f;
   else return gelu_grad(x);
 }
 __device__ __forceinline__ float gelu_grad(float x) {
@@ -922,7 +929,7 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
   if (!dtd_gemm_bt_supported(M, N, K)) return (int)hipErrorInvalidValue;
   if ((lda | ldb | ldc) % 8 || (u && ldu % 8)) return (int)hipErrorInvalidValue;
   if (lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
-  if (epi < EPI_STORE || epi > EPI_GELU_TANH_BWD) return (int)hipErrorInvalidValue;
+  if (epi < EPI_STORE || epi > EPI_RELU_BWD) return (int)hipErrorInvalidValue;
   if (is_gelu_fwd(epi) && !c2) return (int)hipErrorInvalidValue;
   if (is_gelu_bwd(epi) && !u) return (int)hipErrorInvalidValue;
   GemmArgs g{(const bf16*)a, (const bf16*)b, (bf16*)c, (bf16*)c2, (const bf16*)u, (const bf16*)bias, part,
@@ -939,6 +946,8 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
       case EPI_ADD: DTD_GEMM_P(EPI_ADD); break;
       case EPI_BIAS_GELU_TANH: DTD_GEMM_P(EPI_BIAS_GELU_TANH); break;
       case EPI_GELU_TANH_BWD: DTD_GEMM_P(EPI_GELU_TANH_BWD); break;
+      case EPI_BIAS_RELU: DTD_GEMM_P(EPI_BIAS_RELU); break;
+      case EPI_RELU_BWD: DTD_GEMM_P(EPI_RELU_BWD); break;
       default: return (int)hipErrorInvalidValue;
     }
 #undef DTD_GEMM_P
@@ -952,6 +961,8 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
     case EPI_ADD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_ADD>, grid, dim3(512), 0, s, g); break;
     case EPI_BIAS_GELU_TANH: hipLaunchKernelGGL(gemm_bt_kernel<EPI_BIAS_GELU_TANH>, grid, dim3(512), 0, s, g); break;
     case EPI_GELU_TANH_BWD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_GELU_TANH_BWD>, grid, dim3(512), 0, s, g); break;
+    case EPI_BIAS_RELU: hipLaunchKernelGGL(gemm_bt_kernel<EPI_BIAS_RELU>, grid, dim3(512), 0, s, g); break;
+    case EPI_RELU_BWD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_RELU_BWD>, grid, dim3(512), 0, s, g); break;
     default: return (int)hipErrorInvalidValue;
   }
   DTD_LAUNCH_CHECK();

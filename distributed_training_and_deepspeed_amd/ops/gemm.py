@@ -27,10 +27,13 @@ import torch
 
 from . import _lib
 
-EPI_STORE, EPI_BIAS_GELU, EPI_GELU_BWD, EPI_ADD, EPI_BIAS_GELU_TANH, EPI_GELU_TANH_BWD = 0, 1, 2, 3, 4, 5
-# activations with a fused GEMM epilogue: erf GELU (BERT) and its tanh approximation (GPT-2 /
-# BLOOM "gelu_new")
-FUSED_ACTS = ("gelu", "gelu_tanh")
+EPI_STORE, EPI_BIAS_GELU, EPI_GELU_BWD, EPI_ADD = 0, 1, 2, 3
+EPI_BIAS_GELU_TANH, EPI_GELU_TANH_BWD, EPI_BIAS_RELU, EPI_RELU_BWD = 4, 5, 6, 7
+# activations with fused GEMM epilogues: erf GELU (BERT), its tanh approximation (GPT-2 / BLOOM
+# "gelu_new") and ReLU (OPT) -> (forward epilogue, backward epilogue)
+_ACT_EPI = {"gelu": (EPI_BIAS_GELU, EPI_GELU_BWD), "gelu_tanh": (EPI_BIAS_GELU_TANH, EPI_GELU_TANH_BWD),
+            "relu": (EPI_BIAS_RELU, EPI_RELU_BWD)}
+FUSED_ACTS = tuple(_ACT_EPI)
 
 # DTD_GEMM=0 keeps every product on hipBLASLt (A/B runs); the model path checks ``enabled()``.
 _ENABLED = [os.environ.get("DTD_GEMM", "1") == "1"]
@@ -110,20 +113,20 @@ def matmul_nt_add_(c: torch.Tensor, a: torch.Tensor, b_t: torch.Tensor) -> torch
 
 
 def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, act: str = "gelu"):
-    """(u, a) = (x W^T + b, gelu(u)) in one kernel (GELU of the stored bf16 u, as the unfused
-    activation kernel computes it); ``act`` "gelu" (erf) or "gelu_tanh"."""
+    """(u, a) = (x W^T + b, act(u)) in one kernel (the activation of the stored bf16 u, as the
+    unfused activation kernel computes it); ``act`` one of FUSED_ACTS."""
     assert act in FUSED_ACTS, act
     M, N = x.shape[0], w.shape[0]
     u = torch.empty((M, N), dtype=x.dtype, device=x.device)
     a = torch.empty_like(u)
-    _call(EPI_BIAS_GELU if act == "gelu" else EPI_BIAS_GELU_TANH, x, w, u, c2=a, bias=b)
+    _call(_ACT_EPI[act][0], x, w, u, c2=a, bias=b)
     return u, a
 
 
 def gelu_bwd_gemm(dy: torch.Tensor, w_t: torch.Tensor, u: torch.Tensor, dbias=None, act: str = "gelu"):
-    """du = bf16(dy . w_t^T) * gelu'(u); ``w_t`` is the down-projection weight transposed to
+    """du = bf16(dy . w_t^T) * act'(u); ``w_t`` is the down-projection weight transposed to
     [ffn, hidden] (K-contiguous).  ``dbias`` (dst, acc) receives the column sums of du; ``act``
-    "gelu" (erf) or "gelu_tanh"."""
+    one of FUSED_ACTS."""
     assert act in FUSED_ACTS, act
     from .functional import _finalize
     M, N = dy.shape[0], w_t.shape[0]
@@ -132,7 +135,7 @@ def gelu_bwd_gemm(dy: torch.Tensor, w_t: torch.Tensor, u: torch.Tensor, dbias=No
     if dbias is not None:
         nrows = _lib.lib().dtd_gemm_bt_part_rows(M)
         part = torch.empty((nrows, N), dtype=torch.float32, device=dy.device)
-    _call(EPI_GELU_BWD if act == "gelu" else EPI_GELU_TANH_BWD, dy, w_t, du, u=u, part=part)
+    _call(_ACT_EPI[act][1], dy, w_t, du, u=u, part=part)
     if part is not None:
         dst, acc = dbias
         _finalize(part, part.shape[0], N, (dst, acc), acc)

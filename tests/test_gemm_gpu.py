@@ -36,12 +36,16 @@ def test_gemm_bt_asymmetric_operands_detect_transpose():
 
 
 def _gelu_ref(x, act):
+    if act == "relu":
+        return torch.relu(x)
     if act == "gelu":
         return 0.5 * x * (1 + torch.erf(x / 2 ** 0.5))
     return 0.5 * x * (1 + torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3)))
 
 
 def _gelu_grad_ref(x, act):
+    if act == "relu":
+        return (x > 0).float()
     if act == "gelu":
         return 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
     k = 0.7978845608028654
@@ -49,7 +53,7 @@ def _gelu_grad_ref(x, act):
     return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k * (1 + 3 * 0.044715 * x * x)
 
 
-@pytest.mark.parametrize("act", ["gelu", "gelu_tanh"])
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "relu"])
 def test_linear_gelu_epilogue(act):
     torch.manual_seed(1)
     M, N, K = 512, 3072, 768
@@ -67,7 +71,7 @@ def test_linear_gelu_epilogue(act):
     assert rel(a, _gelu_ref(u.float(), act)) < 1e-2
 
 
-@pytest.mark.parametrize("act", ["gelu", "gelu_tanh"])
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "relu"])
 def test_gelu_bwd_gemm_epilogue_and_bias_grad(act):
     torch.manual_seed(2)
     M, H, F = 512, 768, 3072
