@@ -463,7 +463,14 @@ __global__ void __launch_bounds__(512, 2) gemm_tn_kernel(TnArgs g) {
   const int li = lane & 15, lq = lane >> 4;
   const int wm = w >> 2, wn = w & 3;
   const int ntn = g.N / BN;
-  const int tile = blockIdx.x / g.splits, sp = blockIdx.x % g.splits;
+  // XCD-aware order: each XCD runs a contiguous range of (split, tile) with the tile index minor,
+  // so the tiles of one split -- which all stream the same K rows of A and B -- share that
+  // XCD's L2.  In hardware order (tile-major over the splits) every XCD fetched every split's
+  // rows: ~(M/256 + N/256) x the operand bytes from HBM, which bounded the kernel (qkv wgrad:
+  // 3.6 GB in 0.58 ms).
+  const int ntiles = (g.M / BM) * (g.N / BN);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = L % ntiles, sp = L / ntiles;
   const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
   const int nk_all = g.K / BK;
   const int kb = sp * g.ksplit;
@@ -499,6 +506,22 @@ __global__ void __launch_bounds__(512, 2) gemm_tn_kernel(TnArgs g) {
   // 4 columns 4 (li & 3) .. + 3 of a 16-column block; lane receives column li of those rows
   const int trow = 8 * lq + (li >> 2);
   const int tcol = 4 * (li & 3);
+  // The swizzle of every row this lane reads (ks * 32 + trow, + 4) depends on row bits 0, 1 and
+  // 3 only -- one lane constant -- so the 12 swizzled operand offsets are computed once and each
+  // transposing read is base + immediate (per-read XOR / shift address math in the phases kept
+  // the partner wave's MFMAs waiting).
+  const int sw = tn_swz(trow);
+  int aoff[8], boff[4];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int col = wm * 128 + c * 16 + tcol;
+    aoff[c] = trow * 512 + (((col >> 3) ^ sw) << 4) + (col & 7) * 2;
+  }
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int col = wn * 64 + ni * 16 + tcol;
+    boff[ni] = trow * 512 + A_BYTES + (((col >> 3) ^ sw) << 4) + (col & 7) * 2;
+  }
   bf16x8 af[4], bk[4];
   for (int kt = 0; kt < nk; ++kt) {
     const char* cur = smem + (kt & 1) * TILE_BYTES;
@@ -508,36 +531,36 @@ __global__ void __launch_bounds__(512, 2) gemm_tn_kernel(TnArgs g) {
     for (int p = 0; p < 4; ++p) {
       const int ks = p >> 1, qm = (p == 1 || p == 2) ? 1 : 0;
       {
-        const int t0 = ks * 32 + trow, t1 = t0 + 4;
-        const char* r0 = cur + t0 * 512;
-        const char* r1 = cur + t1 * 512;
-        const int s0 = tn_swz(t0), s1 = tn_swz(t1);
+        const char* r0 = cur + ks * 32 * 512;   // rows ks*32 + trow (in the offsets) and + 4
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
-          const int col = wm * 128 + (qm * 4 + mi) * 16 + tcol;
-          const int cb = (col & 7) * 2;
-          af[mi] = __builtin_shufflevector(tr_read(r0 + (((col >> 3) ^ s0) << 4) + cb),
-                                           tr_read(r1 + (((col >> 3) ^ s1) << 4) + cb), 0, 1, 2, 3, 4, 5, 6, 7);
+          const char* q = r0 + aoff[qm * 4 + mi];
+          af[mi] = __builtin_shufflevector(tr_read(q), tr_read(q + 4 * 512), 0, 1, 2, 3, 4, 5, 6, 7);
         }
         if (p == 0 || p == 2) {
 #pragma unroll
           for (int ni = 0; ni < 4; ++ni) {
-            const int col = wn * 64 + ni * 16 + tcol;
-            const int cb = (col & 7) * 2;
-            bk[ni] = __builtin_shufflevector(tr_read(r0 + A_BYTES + (((col >> 3) ^ s0) << 4) + cb),
-                                             tr_read(r1 + A_BYTES + (((col >> 3) ^ s1) << 4) + cb), 0, 1, 2, 3, 4, 5, 6,
-                                             7);
+            const char* q = r0 + boff[ni];
+            bk[ni] = __builtin_shufflevector(tr_read(q), tr_read(q + 4 * 512), 0, 1, 2, 3, 4, 5, 6, 7);
           }
         }
       }
+      // Counted waits retire exactly what this phase reads (2 LDS-DMA instructions per quarter,
+      // completing in issue order): phase 0 needs quarters 0 and 1 of this K-step, phase 1
+      // quarter 0, phase 2 quarters 2 and 3, phase 3 quarter 2.  With the next K-step's quarter
+      // p issued first, that leaves 3 / 4 / 3 / 5 quarters in flight (a blanket vmcnt(4) made
+      // every quarter land 2 phases after issue, which the strided row DMA often did not).
       if (more) {
         if (p == 0) stage_tn<0>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, nxt, kt + 1);
         if (p == 1) stage_tn<1>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, nxt, kt + 1);
         if (p == 2) stage_tn<2>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, nxt, kt + 1);
         if (p == 3) stage_tn<3>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, nxt, kt + 1);
+        if (p == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (p == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (p == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (p == 3) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      } else if (p <= 1) {
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else if (p == 0) {
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
