@@ -71,13 +71,17 @@ struct Pool {
       f();
     }
   }
-  // split [0, n) into chunks over the workers; returns the job id (wait() on it)
+  // split [0, n) into chunks over the workers; returns the job id (wait() on it).  Ids are slots
+  // of a ring: a submit that lands on a slot whose job is still running first waits for it, so
+  // that job's finishing tasks can never count down the new job (callers keep a few jobs in
+  // flight, far below the ring size, so this wait does not happen in practice).
   int submit(int64_t n, const std::function<void(int64_t, int64_t)>& body) {
     const int nt = std::max<int>(1, (int)threads.size());
     const int64_t chunks = std::min<int64_t>(n, nt * 4);
-    std::lock_guard<std::mutex> g(mu);
+    std::unique_lock<std::mutex> g(mu);
     const int job = next_job;
     next_job = (next_job + 1) % (int)pending_per_job.size();
+    done_cv.wait(g, [this, job] { return pending_per_job[job] <= 0; });
     pending_per_job[job] = (int)std::max<int64_t>(chunks, 0);
     for (int64_t c = 0; c < chunks; ++c) {
       const int64_t a = n * c / chunks, b = n * (c + 1) / chunks;

@@ -94,6 +94,22 @@ def test_producer_gather_matches_index_select(threads):
         p.gather(src, torch.tensor([97]), dst)
 
 
+def test_producer_job_ring_wraps_safely():
+    """More jobs than ring slots in flight: every job's rows are complete when its wait returns."""
+    p = BatchProducer(2)
+    src = torch.arange(64 * 16, dtype=torch.int64).view(64, 16)
+    outs, jobs = [], []
+    for k in range(300):                       # > 256 ring slots, none waited until the end
+        idx = torch.tensor([(k + i) % 64 for i in range(8)])
+        dst = torch.empty(8, 16, dtype=torch.int64)
+        jobs.append(p.gather(src, idx, dst, wait=False))
+        outs.append((idx, dst))
+    for j in jobs:
+        p.wait(j)
+    for idx, dst in outs:
+        assert torch.equal(dst, src.index_select(0, idx))
+
+
 def test_native_synthetic_masking_law_and_determinism():
     cfg = C.get_config("base")
     ds = NativeSyntheticLM(cfg, 4096, seq_len=128, seed=11)
