@@ -142,3 +142,27 @@ def test_wgrad_tn_asymmetric_detects_transpose():
     x = torch.arange(T * n, device="cuda").float().view(T, n).remainder(13).bfloat16()
     part = G.wgrad_tn(dy, x, 1)
     assert torch.equal(part[0], x.float())       # I^T x = x (exact small integers)
+
+
+def test_tn_wgrad_path_in_model_matches_default():
+    """The opt-in TN weight-gradient kernel (DTD_GEMM_WGRAD=1; taken for the small o-projection
+    weight at >= 8192 tokens) gives the same gradients as the default hipBLASLt split-K path."""
+    from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
+    from distributed_training_and_deepspeed_amd.models import build_model
+    grads = []
+    for on in (False, True):
+        G._WGRAD[0] = on
+        try:
+            model = build_model("bert-base-cased", dtype=torch.bfloat16, device="cuda", seed=11)
+            ds = SyntheticLMDataset(model.cfg, 16, seq_len=512, seed=2)          # 8192 tokens
+            model(ds.input_ids.cuda(), labels=ds.labels.cuda()).loss.backward()
+            torch.cuda.synchronize()
+            grads.append({n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None})
+        finally:
+            G._WGRAD[0] = False
+    assert grads[0].keys() == grads[1].keys()
+    for n in grads[0]:
+        g0, g1 = grads[0][n], grads[1][n]
+        err = ((g0 - g1).norm() / (g0.norm() + 1e-12)).item()
+        assert err < 2e-2, (n, err)
+    assert sum(n.endswith(".o_w") for n in grads[0]) == 12      # the weights the TN path takes
