@@ -17,6 +17,8 @@ model/transformer.py:18-106 (see ``models/transformer_block.py`` for the hookabl
 """
 from __future__ import annotations
 
+import os
+
 import math
 
 import torch
@@ -197,6 +199,10 @@ class TransformerLayer(nn.Module):
         return x
 
 
+# qkv bias gradient from the attention-backward epilogues (DTD_ATTN_QKV_BIAS=0: separate pass)
+_FUSED_QKV_BIAS = [os.environ.get("DTD_ATTN_QKV_BIAS", "1") == "1"]
+
+
 def _acc(p):
     return grad_dst(p)
 
@@ -323,8 +329,13 @@ class _FusedLayerFn(torch.autograd.Function):
                 grad_done(p)
         emit_wgrad(o_w, do, actx, async_ok=True)
         dctx = do @ o_w
-        dqkv = A.attn_bwd(dctx, qkv, actx, lse, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, ctx.amask)
-        Fx.bias_grad(dqkv, *_pair(qkv_b))
+        # the qkv bias gradient comes out of the attention-backward epilogues (column partials)
+        if _FUSED_QKV_BIAS[0]:
+            dqkv = A.attn_bwd(dctx, qkv, actx, lse, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, ctx.amask,
+                              dbias=_pair(qkv_b))
+        else:
+            dqkv = A.attn_bwd(dctx, qkv, actx, lse, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, ctx.amask)
+            Fx.bias_grad(dqkv, *_pair(qkv_b))
         grad_done(qkv_b)
         if c.pre_ln:
             emit_wgrad(qkv_w, dqkv, a_in, async_ok=True)

@@ -55,7 +55,7 @@ _SIGS = {
     "dtd_sqnorm_partials": (I, [P, I, SZ, P, P]),
     # attention.hip
     "dtd_attn_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, U32, P]),
-    "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
+    "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, P]),
     "dtd_attn_masks": (I, [P, I, I, I, F, P, U32, P]),
     # softmax.hip
     "dtd_softmax_fwd": (I, [I, P, P, I, I, P]),

@@ -178,10 +178,17 @@ def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | 
     return ctx, lse, masks
 
 
-def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, rng=None, sid=0, masks=None):
-    """Returns dqkv [B*S, 3*H*D] in the qkv layout."""
+def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, rng=None, sid=0, masks=None,
+             dbias=None):
+    """Returns dqkv [B*S, 3*H*D] in the qkv layout.  ``dbias`` = (dst, acc): also writes the
+    column sums of dqkv (the qkv projection's bias gradient) -- on the kernel path as per-wave
+    partials from the dQ / dK,dV epilogues (no extra pass over dqkv)."""
+    from . import functional as Fx
     if not kernel_supported(qkv, D):
-        return attn_bwd_ref(dctx, qkv, ctx, lse, B, S, H, D, causal, slopes, p, rng, sid)
+        dqkv = attn_bwd_ref(dctx, qkv, ctx, lse, B, S, H, D, causal, slopes, p, rng, sid)
+        if dbias is not None:
+            Fx.bias_grad(dqkv, *dbias)
+        return dqkv
     dctx = dctx.contiguous()
     dqkv = torch.empty_like(qkv)
     delta = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
@@ -189,7 +196,18 @@ def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, 
     ld = 3 * H * D
     es = qkv.element_size()
     qb, gb = qkv.data_ptr(), dqkv.data_ptr()
+    part = None
+    if dbias is not None and D == 64:
+        # one row per (batch, 32-row block of a 128-row workgroup tile); every entry is written
+        part = torch.empty((B * 4 * ((S + 127) // 128), ld), dtype=torch.float32, device=qkv.device)
     _lib.call("dtd_attn_bwd", qb, qb + H * D * es, qb + 2 * H * D * es, ctx.data_ptr(), dctx.data_ptr(),
               lse.data_ptr(), delta.data_ptr(), _lib.ptr(masks), gb, gb + H * D * es, gb + 2 * H * D * es,
-              _lib.ptr(sl), B, S, H, D, ld, H * D, int(causal), 1.0 / math.sqrt(D), float(p), _lib.stream())
+              _lib.ptr(sl), B, S, H, D, ld, H * D, int(causal), 1.0 / math.sqrt(D), float(p), _lib.ptr(part),
+              _lib.stream())
+    if dbias is not None:
+        if part is not None:
+            dst, acc = dbias
+            Fx._finalize(part, part.shape[0], ld, (dst, acc), acc)
+        else:
+            Fx.bias_grad(dqkv, *dbias)
     return dqkv

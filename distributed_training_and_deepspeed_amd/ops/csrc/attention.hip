@@ -521,7 +521,42 @@ struct BwdArgs {
   const uint32_t* maskA; const uint32_t* maskB;  // dropout keep bits (see attn_mask_kernel)
   int B, S, H, ld, ldo, causal, W;
   float scale, p;
+  // optional [B * 4 * ceil(S/128)][3 H D] fp32 column partials of dqkv (the qkv bias gradient):
+  // one row per (batch, 32-row block of a wave), finished by colsum_finalize
+  float* bias_part;
 };
+
+// Column sums of a wave's 32 rows x 64 columns of dQ / dK / dV, straight from the accumulators
+// (lane r = row of its half-wave, register k = 16 d + i = column d*32 + crow(i, half)): a
+// butterfly reduce-scatter over the 32 lanes of each half (ds_swizzle lane ^ s) leaves the sum of
+// column index k = r in lane r -- 31 exchanges instead of 32 x 5 -- and one store per wave writes
+// the 64 column partials.  This replaces a separate pass over the 3 H D-wide gradient (the qkv
+// bias gradient: ~90 us a layer at b256 x 512).
+template <int S_>
+__device__ __forceinline__ float xswz(float x) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), (S_ << 10) | 0x1f));
+}
+template <int S_, int N>
+__device__ __forceinline__ void rs_step(const float (&in)[2 * N], float (&out)[N], int r) {
+  const bool hi = (r & S_) != 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const float mine = hi ? in[j + N] : in[j];
+    const float other = hi ? in[j] : in[j + N];
+    out[j] = mine + xswz<S_>(other);
+  }
+}
+__device__ __forceinline__ float colsum32(const float (&v)[32], int r) {
+  float a16[16], a8[8], a4[4], a2[2], a1[1];
+  rs_step<16, 16>(v, a16, r);
+  rs_step<8, 8>(a16, a8, r);
+  rs_step<4, 4>(a8, a4, r);
+  rs_step<2, 2>(a4, a2, r);
+  rs_step<1, 1>(a2, a1, r);
+  return a1[0];
+}
+// column (within the head) of register index k = 16 d + i in lane half hh
+__device__ __forceinline__ int colsum_col(int k, int hh) { return (k >> 4) * 32 + crow(k & 15, hh); }
 
 // dK, dV: grid (ceil(S/128), B*H); block 256 = 4 waves x 32 keys ("key on the lane").
 // Query tiles of 64 rows (Q, dO row-major in LDS, double-buffered).
@@ -699,8 +734,22 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
     }
     __syncthreads();
   }
-  if (!kvalid) return;
   const float dv_scale = inv_keep;   // the dropped P fed to dV carried keep bits only
+  if (a.bias_part && D == 64) {
+    float vk[32], vv[32];
+#pragma unroll
+    for (int d = 0; d < NDB; ++d)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {   // the stored (bf16-rounded) values, 0 past S
+        vk[16 * d + i] = kvalid ? (float)(bf16)(dk[d][i] * a.scale) : 0.f;
+        vv[16 * d + i] = kvalid ? (float)(bf16)(dv[d][i] * dv_scale) : 0.f;
+      }
+    const float sk = colsum32(vk, r), sv = colsum32(vv, r);
+    float* row = a.bias_part + ((size_t)b * gridDim.x * 4 + (kblk >> 5) + w) * (3 * a.H * D) + h * D + colsum_col(r, hh);
+    row[a.H * D] = sk;
+    row[2 * a.H * D] = sv;
+  }
+  if (!kvalid) return;
   bf16* dkp = a.dk + (size_t)(b * S + key) * a.ld + h * D;
   bf16* dvp = a.dv + (size_t)(b * S + key) * a.ld + h * D;
 #pragma unroll
@@ -862,6 +911,15 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
     tile(std::integral_constant<int, 1>{}, t);
     if (t + 1 < nt) tile(std::integral_constant<int, 0>{}, t + 1);
   }
+  if (a.bias_part && D == 64) {
+    float vq[32];
+#pragma unroll
+    for (int d = 0; d < NDB; ++d)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) vq[16 * d + i] = qvalid ? (float)(bf16)(dq[d][i] * a.scale) : 0.f;
+    const float sq = colsum32(vq, r);
+    a.bias_part[((size_t)b * gridDim.x * 4 + (qblk >> 5) + w) * (3 * a.H * D) + h * D + colsum_col(r, hh)] = sq;
+  }
   if (!qvalid) return;
   bf16* qp = a.dq + (size_t)(b * S + q) * a.ld + h * D;
 #pragma unroll
@@ -976,7 +1034,7 @@ static void launch_dkdv(dim3 grid, hipStream_t s, const BwdArgs& a) {
 DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                             const float* lse, float* delta, const uint32_t* masks, void* dq, void* dk, void* dv,
                             const float* slopes, int B, int S, int H, int D, int ld, int ldo, int causal, float scale,
-                            float p, hipStream_t s) {
+                            float p, float* bias_part, hipStream_t s) {
   if (B * S * H == 0) return 0;
   if (D != 64 && D != 128) return (int)hipErrorInvalidValue;
   if (!offsets_fit(S, ld, ldo)) return (int)hipErrorInvalidValue;
@@ -986,7 +1044,8 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   if (p > 0.f && !masks) return (int)hipErrorInvalidValue;
   dim3 grid((S + 127) / 128, B * H);
   BwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (const bf16*)o,
-            (bf16*)dq, (bf16*)dk, (bf16*)dv, slopes, mA, mB, B, S, H, ld, ldo, causal, W, scale, p};
+            (bf16*)dq, (bf16*)dk, (bf16*)dv, slopes, mA, mB, B, S, H, ld, ldo, causal, W, scale, p,
+            D == 64 ? bias_part : nullptr};
   // dQ first: it also produces delta = rowsum(dO * O), which the dK/dV kernel then reads
   if (D == 64) {
     const int o = occupancy(2);

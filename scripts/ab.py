@@ -75,7 +75,7 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "no_gemm": _env(DTD_GEMM="0"), "gemm_bwd_only": _env(DTD_GEMM_FFN_FWD="0"),
            "gemm_fwd_only": _env(DTD_GEMM_FFN_BWD="0"), "gemm_tile": _env(DTD_GEMM_VARIANT="0"),
            "no_gemm_wgrad": _env(DTD_GEMM_WGRAD="0"), "gemm_wgrad": _env(DTD_GEMM_WGRAD="1"),
-           "mask_ballot": _env(DTD_ATTN_MASK="0"),
+           "mask_ballot": _env(DTD_ATTN_MASK="0"), "no_qkv_bias_fused": _env(DTD_ATTN_QKV_BIAS="0"),
            "base_so": _env(DTD_KERNELS_SO=os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops",
                                                       "_dtd_kernels_base.so"))}
 

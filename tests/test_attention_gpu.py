@@ -49,6 +49,13 @@ def test_flash_attention_fwd_bwd(B, S, H, D, causal, alibi, p):
     for i, name in enumerate("qkv"):
         e = rel(g[:, :, i], r[:, :, i])
         assert e < 2e-2, f"d{name} rel err {e}"
+    # qkv bias gradient from the backward epilogues (column partials) == column sums of dqkv
+    db = torch.full((3 * H * D,), 0.25, device="cuda", dtype=torch.float32)
+    dq_b = A.attn_bwd(dctx.cuda(), qkv.cuda(), ctx_g, lse_g, B, S, H, D, causal, slopes, p, rg, 9, mk,
+                      dbias=(db, True))
+    assert torch.equal(dq_b, dq_g)
+    ref_db = dq_g.float().sum(0)
+    assert ((db - 0.25) - ref_db).abs().max().item() <= 1e-3 * (ref_db.abs().max().item() + 1.0)
 
 
 def test_side_stream_masks_match_inline_generation():
