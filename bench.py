@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--reduce-bucket", type=float, default=2.5e7,
                     help="ZeRO reduce_bucket_size (elements) for --zero-stage")
     ap.add_argument("--dense-mlm-head", action="store_true")
+    ap.add_argument("--mlm-capacity", default="static", choices=["static", "dynamic"],
+                    help="sparse MLM head rows: a fixed capacity (mean + 8 sigma of the 15%% law, rounded "
+                         "to 256; constant GEMM shapes, no per-step host sync; overflow raises) or the exact "
+                         "labelled-row count per batch")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
     return ap.parse_args()
@@ -132,11 +136,18 @@ def main():
         model.rt.rng.advance()
         return out.loss.detach()
 
+    static_mlm = mlm and not args.dense_mlm_head and cuda and (args.graph == "on" or args.mlm_capacity == "static")
+    if static_mlm:
+        # fixed labelled-row capacity: padding rows carry label -100 (zero loss and gradient), so
+        # loss and gradients equal the exact-count head's; rt.mlm_overflow flags a batch that
+        # would not fit (checked after the timed steps)
+        from distributed_training_and_deepspeed_amd.utils.graphs import mlm_capacity
+        model.rt.mlm_capacity = -(-mlm_capacity(B * S) // 256) * 256
+        model.rt.mlm_overflow = torch.zeros((), dtype=torch.bool, device=device)
     graphed = None
     if args.graph == "on" and cuda and not zero:
         # one hipGraph replay per step (host-launch-bound small batches); static-size MLM head
-        from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep, mlm_capacity
-        model.rt.mlm_capacity = mlm_capacity(B * S)
+        from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep
         graphed = CapturedStep(train_step, {"input_ids": ids[0], "labels": labels[0]}, warmup=3, runtime=model.rt)
 
     def step(i):
@@ -162,6 +173,8 @@ def main():
     dt = time.perf_counter() - t0
     if graphed is not None:
         graphed.check()
+    if static_mlm and bool(model.rt.mlm_overflow):
+        raise RuntimeError("a batch had more labelled rows than the static MLM capacity: use --mlm-capacity dynamic")
     if world > 1:
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -196,6 +209,8 @@ def main():
                 "grad_dtype": str(gdt).replace("torch.", ""),
                 "impl": args.impl,
                 "mlm_head": (None if not mlm else "dense" if args.dense_mlm_head
+                             else "sparse (labelled rows only, static capacity %d; identical loss/grads)"
+                             % model.rt.mlm_capacity if static_mlm
                              else "sparse (labelled rows only; identical loss/grads)"),
                 "optimizer": ("fused Adam on the ZeRO shard (zero_dp_training.py config, lr 1.5e-4)" if zero
                               else "fused AdamW (transformers.AdamW hyper-params, lr 5e-5)"),

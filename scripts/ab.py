@@ -57,7 +57,7 @@ def _mlm_static():
 
     def init(self, *a, **k):
         orig(self, *a, **k)
-        self.mlm_capacity = mlm_capacity(128 * 512)
+        self.mlm_capacity = -(-mlm_capacity(int(os.environ.get("DTD_BENCH_BATCH", "256")) * 512) // 256) * 256
     T.Runtime.__init__ = init
 
 
@@ -67,7 +67,7 @@ def _env(**kv):
     return f
 
 
-PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned, "mlm_static": _mlm_static, "graph": lambda: ["--graph", "on"],
+PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned, "mlm_static": _mlm_static, "mlm_dynamic": lambda: ["--mlm-capacity", "dynamic"], "graph": lambda: ["--graph", "on"],
            "attn_occ_323": _env(DTD_ATTN_OCC="3,2,3"), "attn_occ_222_dq64": _env(DTD_ATTN_TILE="64,64"),
            "attn_occ_322": _env(DTD_ATTN_OCC="3,2,2"), "attn_occ_323_dq64": _env(DTD_ATTN_OCC="3,2,3", DTD_ATTN_TILE="64,64"),
            "base": lambda: None, "old_wgrad_split": _old_wgrad_split, "f32_wgrad_partials": _f32_wgrad_partials,
