@@ -41,8 +41,10 @@ def default_backend() -> str:
 
 def init(rank: int | None = None, world_size: int | None = None, backend: str | None = None,
          master_addr: str | None = None, master_port: int | str | None = None, local_rank: int | None = None,
-         timeout_s: float = 1800.0) -> tuple[int, int]:
-    """Initialise the default process group (idempotent).  Returns (rank, world_size)."""
+         timeout_s: float = 1800.0, init_method: str | None = None) -> tuple[int, int]:
+    """Initialise the default process group (idempotent).  Returns (rank, world_size).
+    ``init_method`` (e.g. ``file:///tmp/x/rdzv``) replaces the TCP rendezvous on MASTER_ADDR /
+    MASTER_PORT -- single-host jobs that must not race for a port (tests)."""
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     rank = env_rank() if rank is None else rank
@@ -59,6 +61,8 @@ def init(rank: int | None = None, world_size: int | None = None, backend: str | 
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
         kw["device_id"] = torch.device("cuda", local_rank)
+    if init_method is not None:
+        kw["init_method"] = init_method
     dist.init_process_group(backend=backend, rank=rank, world_size=world_size,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return rank, world_size

@@ -51,7 +51,7 @@ def _ipc_rank(rank, world, port, out):
     """Real (IPC) mode: `world` processes on the same GPU map each other's staging and signal buffers
     through hipIpcOpenMemHandle, exactly as ranks on different GPUs of a node do."""
     from distributed_training_and_deepspeed_amd import comm
-    comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
+    comm.init(rank=rank, world_size=world, backend="gloo", init_method=f"file://{out}/rdzv")
     torch.cuda.set_device(0)
     ar = XgmiAllReduce(max_bytes=4 << 20, one_shot_max=64 << 10, blocks=8)
     ok = True
