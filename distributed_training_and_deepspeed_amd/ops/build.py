@@ -63,6 +63,19 @@ def _compile(src: Path, hipcc: str, extra: list[str]) -> Path:
     return obj
 
 
+def _check_kernel_stubs(lib: Path) -> None:
+    """Refuse a library with unresolved kernel launch stubs: hipcc can drop a ``__global__``
+    template's host stub without an error (e.g. a lambda inside the kernel body), which only
+    surfaces as an ``undefined symbol`` when the library is loaded on the GPU box."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not Path(nm).exists():
+        return
+    r = subprocess.run([nm, "-D", "--undefined-only", str(lib)], capture_output=True, text=True)
+    bad = [ln.split()[-1] for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+    if bad:
+        raise RuntimeError(f"{lib.name}: unresolved kernel stubs (host side of a kernel was not emitted): {bad}")
+
+
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
     """Compile all kernels for gfx950 and link ``_dtd_kernels.so`` in-tree; return its path."""
     if not force and not needs_build():
@@ -82,6 +95,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    _check_kernel_stubs(tmp)
     os.replace(tmp, LIB_PATH)
     if verbose:
         print(f"[dtd.build] wrote {LIB_PATH}", file=sys.stderr)

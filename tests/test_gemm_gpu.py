@@ -53,10 +53,13 @@ def _gelu_grad_ref(x, act):
     return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k * (1 + 3 * 0.044715 * x * x)
 
 
+# (8448, 768) / (16384, 768) / (8448, 512): more tiles than workgroups, so every persistent
+# workgroup runs several epilogues back to back (uneven tile counts per workgroup)
+@pytest.mark.parametrize("M,K", [(512, 768), (8448, 768), (16384, 768), (8448, 512)])
 @pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "relu"])
-def test_linear_gelu_epilogue(act):
+def test_linear_gelu_epilogue(act, M, K):
     torch.manual_seed(1)
-    M, N, K = 512, 3072, 768
+    N = 3072
     x = torch.randn(M, K, device="cuda").bfloat16()
     w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
     b = torch.randn(N, device="cuda").bfloat16()
