@@ -249,8 +249,15 @@ class _FusedLayerFn(torch.autograd.Function):
             z1, f_in, m2, r2 = Fx.ln_fwd(o, x2d, g2, b2, eps, p_h, rng, s1)
         else:
             z1, f_in, m1, r1 = Fx.ln_fwd(o, x2d, g1, b1, eps, p_h, rng, s1)
+        ffn_g = False   # u holds act'(pre-activation) instead of the pre-activation
         if G.ffn_fwd_enabled() and _ffn_gemm_ok(c, f_in, w1):
-            u, a = G.linear_gelu(f_in, w1, bf1, c.activation)     # fc1 + bias + GELU in one kernel
+            if rt.keep_ffn_act and c.activation in G.GRAD_ACTS and G.ffn_store_grad_enabled():
+                # fc1 + bias + GELU + GELU' in one kernel: the backward multiplies by the stored
+                # derivative (its exp / rcp shared with the forward GELU here)
+                u, a = G.linear_act_grad(f_in, w1, bf1, c.activation)
+                ffn_g = True
+            else:
+                u, a = G.linear_gelu(f_in, w1, bf1, c.activation)     # fc1 + bias + GELU in one kernel
         else:
             u = F.linear(f_in, w1, bf1)
             a = Fx.act_fwd(u, c.activation)
@@ -269,6 +276,7 @@ class _FusedLayerFn(torch.autograd.Function):
         ctx.amask = amask  # attention dropout keep bits (kernel path) for the backward
         ctx.rng = rng  # the RngState of this forward's device (pipeline stages differ)
         ctx.meta = (B, S, h, H, D, p_h, p_a, sa, s1, s2)
+        ctx.ffn_g = ffn_g
         return out.view(B, S, h)
 
     @staticmethod
@@ -298,7 +306,15 @@ class _FusedLayerFn(torch.autograd.Function):
         if (a is not None and G.ffn_bwd_enabled() and c.activation in G.FUSED_ACTS and dy.is_cuda
                 and dy.dtype == torch.bfloat16 and G.supported(dy.shape[0], w2.shape[1], dy.shape[1], dy, u)):
             w2t = G.transpose(w2)                      # [ffn, hidden]: K-contiguous B operand
-        if w2t is not None:
+        if ctx.ffn_g:
+            # u holds act'(u): dU = dA * u
+            if w2t is not None:
+                du = G.mul_bwd_gemm(dy, w2t, u, dbias=_acc(bf1))
+                del w2t
+            else:
+                du = ((dy @ w2).float() * u.float()).to(dy.dtype)
+                Fx.bias_grad(du, *_pair(bf1))
+        elif w2t is not None:
             # fc2 dgrad, GELU' and fc1's bias gradient in one kernel (no da round trip)
             du = G.gelu_bwd_gemm(dy, w2t, u, dbias=_acc(bf1), act=c.activation)
             del w2t

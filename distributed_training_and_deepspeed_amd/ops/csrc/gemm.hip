@@ -12,6 +12,11 @@
 //   EPI_ADD        C = C + acc (in place)                       residual-branch dgrad (post-LN BERT)
 //   EPI_BIAS_GELU_TANH / EPI_GELU_TANH_BWD, EPI_BIAS_RELU / EPI_RELU_BWD: the same two
 //                  activation epilogues for tanh GELU (GPT-2 / BLOOM "gelu_new") and ReLU (OPT)
+//   EPI_BIAS_GELU_G / EPI_BIAS_GELU_TANH_G   A = act(U) and G = act'(U) (U = acc + bias rounded
+//                  to bf16, as above) from the same exponential; store G in place of U
+//   EPI_MUL_BWD    dU = bf16(acc) * G (G = the stored derivative); column partials of dU.  The
+//                  pair moves the derivative's transcendental math out of the backward epilogue
+//                  (a multiply there) into the forward one, where it shares GELU's exp / rcp
 //
 // Main loop (cdna_hip_programming.md §5, "256² 8-phase template"): 256x256 output tile per
 // 512-thread workgroup, 8 waves as 2 (M) x 4 (N), each wave 128 x 64 as 8 x 4 tiles of
@@ -48,14 +53,18 @@ constexpr int TILE_BYTES = (BM + BN) * BK * 2;   // 64 KiB per K-step buffer
 constexpr int LDS_BYTES = 2 * TILE_BYTES;        // 128 KiB
 
 enum Epi : int { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_GELU_BWD = 2, EPI_ADD = 3, EPI_BIAS_GELU_TANH = 4,
-                 EPI_GELU_TANH_BWD = 5, EPI_BIAS_RELU = 6, EPI_RELU_BWD = 7 };
+                 EPI_GELU_TANH_BWD = 5, EPI_BIAS_RELU = 6, EPI_RELU_BWD = 7, EPI_BIAS_GELU_G = 8,
+                 EPI_BIAS_GELU_TANH_G = 9, EPI_MUL_BWD = 10, EPI_LAST = EPI_MUL_BWD };
 // activation epilogues (the names keep "gelu" for the family: store U and act(U) / act'(U) . dA)
 __host__ __device__ constexpr bool is_gelu_fwd(int e) {
-  return e == EPI_BIAS_GELU || e == EPI_BIAS_GELU_TANH || e == EPI_BIAS_RELU;
+  return e == EPI_BIAS_GELU || e == EPI_BIAS_GELU_TANH || e == EPI_BIAS_RELU || e == EPI_BIAS_GELU_G ||
+         e == EPI_BIAS_GELU_TANH_G;
 }
 __host__ __device__ constexpr bool is_gelu_bwd(int e) {
-  return e == EPI_GELU_BWD || e == EPI_GELU_TANH_BWD || e == EPI_RELU_BWD;
+  return e == EPI_GELU_BWD || e == EPI_GELU_TANH_BWD || e == EPI_RELU_BWD || e == EPI_MUL_BWD;
 }
+// forward activation epilogues that store the derivative G in place of U
+__host__ __device__ constexpr bool stores_grad(int e) { return e == EPI_BIAS_GELU_G || e == EPI_BIAS_GELU_TANH_G; }
 
 struct GemmArgs {
   const bf16* a; const bf16* b;          // A [M, K] (lda), B [N, K] (ldb)
@@ -125,7 +134,7 @@ template <int EPI> __device__ __forceinline__ float epi_act_grad(float x);
 __device__ __forceinline__ float gelu_grad(float x);
 template <int EPI>
 __device__ __forceinline__ float epi_act(float x) {
-  if constexpr (EPI == EPI_BIAS_GELU_TANH) return gelu_tanh(x);
+  if constexpr (EPI == EPI_BIAS_GELU_TANH || EPI == EPI_BIAS_GELU_TANH_G) return gelu_tanh(x);
   else if constexpr (EPI == EPI_BIAS_RELU) return x > 0.f ? x : 0.f;
   else return gelu(x);
 }
@@ -133,7 +142,24 @@ template <int EPI>
 __device__ __forceinline__ float epi_act_grad(float x) {
   if constexpr (EPI == EPI_GELU_TANH_BWD) return gelu_tanh_grad(x);
   else if constexpr (EPI == EPI_RELU_BWD) return x > 0.f ? 1.f : 0.f;
+  else if constexpr (EPI == EPI_MUL_BWD) return x;   // the input already is the derivative
   else return gelu_grad(x);
+}
+// act(x) and act'(x) sharing the transcendental terms (EPI_BIAS_GELU_G / _TANH_G)
+template <int EPI>
+__device__ __forceinline__ void epi_act_and_grad(float x, float& a, float& d) {
+  if constexpr (EPI == EPI_BIAS_GELU_TANH_G) {
+    const float k = 0.7978845608028654f;
+    const float t = tanh_fast(k * fmaf(0.044715f * x, x * x, x));
+    const float h = 0.5f * (1.f + t);
+    a = x * h;
+    d = h + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+  } else {
+    const float e = __expf(-0.5f * x * x);
+    const float cdf = phi_cdf(x, e);
+    a = x * cdf;
+    d = fmaf(x * 0.3989422804014327f, e, cdf);
+  }
 }
 __device__ __forceinline__ float gelu_grad(float x) {
   const float e = __expf(-0.5f * x * x);
@@ -352,6 +378,17 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_kernel(GemmArgs g) {
     const size_t off = (size_t)(m0 + r) * g.ldc + n0 + c * 8;
     if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
       *reinterpret_cast<bf16x8*>(g.c + off) = v;
+    } else if constexpr (stores_grad(EPI)) {
+      bf16x8 a, d;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float aj, dj;
+        epi_act_and_grad<EPI>((float)v[j], aj, dj);
+        a[j] = (bf16)aj;
+        d[j] = (bf16)dj;
+      }
+      *reinterpret_cast<bf16x8*>(g.c + off) = d;
+      *reinterpret_cast<bf16x8*>(g.c2 + off) = a;
     } else if constexpr (is_gelu_fwd(EPI)) {
       bf16x8 a;
 #pragma unroll
@@ -810,6 +847,17 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
         const size_t off = (size_t)(m0 + rr * 128 + r) * g.ldc + n0 + c * 8;
         if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
           *reinterpret_cast<bf16x8*>(g.c + off) = v;
+        } else if constexpr (stores_grad(EPI)) {
+          bf16x8 av, dv;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float aj, dj;
+            epi_act_and_grad<EPI>((float)v[j], aj, dj);
+            av[j] = (bf16)aj;
+            dv[j] = (bf16)dj;
+          }
+          *reinterpret_cast<bf16x8*>(g.c + off) = dv;
+          *reinterpret_cast<bf16x8*>(g.c2 + off) = av;
         } else if constexpr (is_gelu_fwd(EPI)) {
           bf16x8 av;
 #pragma unroll
@@ -952,7 +1000,7 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
   if (!dtd_gemm_bt_supported(M, N, K)) return (int)hipErrorInvalidValue;
   if ((lda | ldb | ldc) % 8 || (u && ldu % 8)) return (int)hipErrorInvalidValue;
   if (lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
-  if (epi < EPI_STORE || epi > EPI_RELU_BWD) return (int)hipErrorInvalidValue;
+  if (epi < EPI_STORE || epi > EPI_LAST) return (int)hipErrorInvalidValue;
   if (is_gelu_fwd(epi) && !c2) return (int)hipErrorInvalidValue;
   if (is_gelu_bwd(epi) && !u) return (int)hipErrorInvalidValue;
   GemmArgs g{(const bf16*)a, (const bf16*)b, (bf16*)c, (bf16*)c2, (const bf16*)u, (const bf16*)bias, part,
@@ -971,6 +1019,9 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
       case EPI_GELU_TANH_BWD: DTD_GEMM_P(EPI_GELU_TANH_BWD); break;
       case EPI_BIAS_RELU: DTD_GEMM_P(EPI_BIAS_RELU); break;
       case EPI_RELU_BWD: DTD_GEMM_P(EPI_RELU_BWD); break;
+      case EPI_BIAS_GELU_G: DTD_GEMM_P(EPI_BIAS_GELU_G); break;
+      case EPI_BIAS_GELU_TANH_G: DTD_GEMM_P(EPI_BIAS_GELU_TANH_G); break;
+      case EPI_MUL_BWD: DTD_GEMM_P(EPI_MUL_BWD); break;
       default: return (int)hipErrorInvalidValue;
     }
 #undef DTD_GEMM_P
@@ -986,6 +1037,9 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
     case EPI_GELU_TANH_BWD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_GELU_TANH_BWD>, grid, dim3(512), 0, s, g); break;
     case EPI_BIAS_RELU: hipLaunchKernelGGL(gemm_bt_kernel<EPI_BIAS_RELU>, grid, dim3(512), 0, s, g); break;
     case EPI_RELU_BWD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_RELU_BWD>, grid, dim3(512), 0, s, g); break;
+    case EPI_BIAS_GELU_G: hipLaunchKernelGGL(gemm_bt_kernel<EPI_BIAS_GELU_G>, grid, dim3(512), 0, s, g); break;
+    case EPI_BIAS_GELU_TANH_G: hipLaunchKernelGGL(gemm_bt_kernel<EPI_BIAS_GELU_TANH_G>, grid, dim3(512), 0, s, g); break;
+    case EPI_MUL_BWD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_MUL_BWD>, grid, dim3(512), 0, s, g); break;
     default: return (int)hipErrorInvalidValue;
   }
   DTD_LAUNCH_CHECK();

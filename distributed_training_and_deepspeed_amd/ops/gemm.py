@@ -11,6 +11,11 @@ input-gradient product uses the transposed weight, ``transpose``):
 * ``gelu_bwd_gemm(dy, w_t, u, dbias)`` -> du = (dy w_t^T) * gelu'(u) plus the column sums of du
                                       (FFN down-projection dgrad with the GELU derivative and the
                                       up-projection's bias gradient in the epilogue)
+* ``linear_act_grad(x, w, b)``     -> (g, a): a = gelu(u) and g = gelu'(u) (u = x W^T + b) from one
+                                      exponential; g is stored instead of u
+* ``mul_bwd_gemm(dy, w_t, g, dbias)`` -> du = (dy w_t^T) * g plus the column sums of du (the
+                                      backward partner of ``linear_act_grad``: a multiply instead of
+                                      the derivative's transcendental math)
 * ``wgrad_tn(dy, x)``              -> fp32 split-K partials of dy^T x (weight gradient of a Linear:
                                       both operands row-major over the token dim, transposing LDS
                                       reads; one wave of workgroups; ``grad.splitk_reduce`` sums)
@@ -29,11 +34,15 @@ from . import _lib
 
 EPI_STORE, EPI_BIAS_GELU, EPI_GELU_BWD, EPI_ADD = 0, 1, 2, 3
 EPI_BIAS_GELU_TANH, EPI_GELU_TANH_BWD, EPI_BIAS_RELU, EPI_RELU_BWD = 4, 5, 6, 7
+EPI_BIAS_GELU_G, EPI_BIAS_GELU_TANH_G, EPI_MUL_BWD = 8, 9, 10
 # activations with fused GEMM epilogues: erf GELU (BERT), its tanh approximation (GPT-2 / BLOOM
 # "gelu_new") and ReLU (OPT) -> (forward epilogue, backward epilogue)
 _ACT_EPI = {"gelu": (EPI_BIAS_GELU, EPI_GELU_BWD), "gelu_tanh": (EPI_BIAS_GELU_TANH, EPI_GELU_TANH_BWD),
             "relu": (EPI_BIAS_RELU, EPI_RELU_BWD)}
 FUSED_ACTS = tuple(_ACT_EPI)
+# activations whose forward epilogue can store the derivative instead of the pre-activation
+_ACT_GRAD_EPI = {"gelu": EPI_BIAS_GELU_G, "gelu_tanh": EPI_BIAS_GELU_TANH_G}
+GRAD_ACTS = tuple(_ACT_GRAD_EPI)
 
 # DTD_GEMM=0 keeps every product on hipBLASLt (A/B runs); the model path checks ``enabled()``.
 _ENABLED = [os.environ.get("DTD_GEMM", "1") == "1"]
@@ -43,6 +52,9 @@ _ENABLED = [os.environ.get("DTD_GEMM", "1") == "1"]
 # the GELU epilogue, and the FFN down-projection dgrad with the GELU-backward epilogue.
 _FFN_FWD = [os.environ.get("DTD_GEMM_FFN_FWD", "1") == "1"]
 _FFN_BWD = [os.environ.get("DTD_GEMM_FFN_BWD", "1") == "1"]
+# The FFN up-projection stores gelu'(u) instead of u (the derivative's exp / rcp shared with the
+# forward GELU; the backward epilogue is a multiply).  One extra bf16 rounding of the derivative.
+_FFN_STORE_GRAD = [os.environ.get("DTD_GEMM_FFN_STORE_GRAD", "1") == "1"]
 # TN weight-gradient kernel: off by default -- even on the o-projection, where it wins in
 # isolation, the full-chip split-K grid on the side stream cost 0.35 % end-to-end
 # (profiles/r2_ab_gemm_oproj.jsonl).  The NT kernel on the transposed o-projection weight (152 vs
@@ -60,6 +72,10 @@ def ffn_fwd_enabled() -> bool:
 
 def ffn_bwd_enabled() -> bool:
     return _ENABLED[0] and _FFN_BWD[0]
+
+
+def ffn_store_grad_enabled() -> bool:
+    return _ENABLED[0] and _FFN_FWD[0] and _FFN_BWD[0] and _FFN_STORE_GRAD[0]
 
 
 def wgrad_enabled() -> bool:
@@ -123,11 +139,32 @@ def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, act: s
     return u, a
 
 
+def linear_act_grad(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, act: str = "gelu"):
+    """(g, a) = (act'(u), act(u)) with u = bf16(x W^T + b), in one kernel; ``act`` one of
+    GRAD_ACTS.  u itself is not stored: the backward takes g (``mul_bwd_gemm``)."""
+    assert act in GRAD_ACTS, act
+    M, N = x.shape[0], w.shape[0]
+    g = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    a = torch.empty_like(g)
+    _call(_ACT_GRAD_EPI[act], x, w, g, c2=a, bias=b)
+    return g, a
+
+
+def mul_bwd_gemm(dy: torch.Tensor, w_t: torch.Tensor, g: torch.Tensor, dbias=None):
+    """du = bf16(dy . w_t^T) * g with g = act'(u) from ``linear_act_grad``; ``dbias`` as in
+    ``gelu_bwd_gemm``."""
+    return _act_bwd_gemm(EPI_MUL_BWD, dy, w_t, g, dbias)
+
+
 def gelu_bwd_gemm(dy: torch.Tensor, w_t: torch.Tensor, u: torch.Tensor, dbias=None, act: str = "gelu"):
     """du = bf16(dy . w_t^T) * act'(u); ``w_t`` is the down-projection weight transposed to
     [ffn, hidden] (K-contiguous).  ``dbias`` (dst, acc) receives the column sums of du; ``act``
     one of FUSED_ACTS."""
     assert act in FUSED_ACTS, act
+    return _act_bwd_gemm(_ACT_EPI[act][1], dy, w_t, u, dbias)
+
+
+def _act_bwd_gemm(epi: int, dy: torch.Tensor, w_t: torch.Tensor, u: torch.Tensor, dbias):
     from .functional import _finalize
     M, N = dy.shape[0], w_t.shape[0]
     du = torch.empty((M, N), dtype=dy.dtype, device=dy.device)
@@ -135,7 +172,7 @@ def gelu_bwd_gemm(dy: torch.Tensor, w_t: torch.Tensor, u: torch.Tensor, dbias=No
     if dbias is not None:
         nrows = _lib.lib().dtd_gemm_bt_part_rows(M)
         part = torch.empty((nrows, N), dtype=torch.float32, device=dy.device)
-    _call(_ACT_EPI[act][1], dy, w_t, du, u=u, part=part)
+    _call(epi, dy, w_t, du, u=u, part=part)
     if part is not None:
         dst, acc = dbias
         _finalize(part, part.shape[0], N, (dst, acc), acc)

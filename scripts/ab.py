@@ -76,6 +76,7 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "gemm_fwd_only": _env(DTD_GEMM_FFN_BWD="0"), "gemm_tile": _env(DTD_GEMM_VARIANT="0"),
            "no_gemm_wgrad": _env(DTD_GEMM_WGRAD="0"), "gemm_wgrad": _env(DTD_GEMM_WGRAD="1"),
            "mask_ballot": _env(DTD_ATTN_MASK="0"), "no_qkv_bias_fused": _env(DTD_ATTN_QKV_BIAS="0"),
+           "no_ffn_store_grad": _env(DTD_GEMM_FFN_STORE_GRAD="0"),
            "base_so": _env(DTD_KERNELS_SO=os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops",
                                                       "_dtd_kernels_base.so"))}
 

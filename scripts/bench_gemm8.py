@@ -92,6 +92,12 @@ def main():
         "dgrad_fc2": (2 * T * H * F, lambda: x @ w["fc2"], lambda: G.matmul_nt(x, wt["fc2"])),
         "dgrad_fc2_gelu_bwd": (2 * T * H * F, lambda: Fx.act_bwd(x @ w["fc2"], u, "gelu", dbias=(db, False)),
                                lambda: G.gelu_bwd_gemm(x, wt["fc2"], u, dbias=(db, False))),
+        # derivative-storing pair (the model default): the forward also emits gelu'(u), the
+        # backward epilogue multiplies (the hipBLASLt column is the same unfused baseline)
+        "fwd_fc1_gelu_grad": (2 * T * H * F, lambda: Fx.act_fwd(L(x, w["fc1"], b["fc1"]), "gelu"),
+                              lambda: G.linear_act_grad(x, w["fc1"], b["fc1"])),
+        "dgrad_fc2_mul_bwd": (2 * T * H * F, lambda: Fx.act_bwd(x @ w["fc2"], u, "gelu", dbias=(db, False)),
+                              lambda: G.mul_bwd_gemm(x, wt["fc2"], u, dbias=(db, False))),
         "transpose_fc1": (0, lambda: None, lambda: G.transpose(w["fc1"])),
     }
     # weight gradients: hipBLASLt split-K (16 x T/16-token slices, bf16 partials) + reduce vs the

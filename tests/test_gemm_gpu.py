@@ -169,3 +169,60 @@ def test_tn_wgrad_path_in_model_matches_default():
         err = ((g0 - g1).norm() / (g0.norm() + 1e-12)).item()
         assert err < 2e-2, (n, err)
     assert sum(n.endswith(".o_w") for n in grads[0]) == 12      # the weights the TN path takes
+
+
+@pytest.mark.parametrize("M", [512, 8448])
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh"])
+def test_act_grad_epilogue_pair_matches_fp32(act, M):
+    """linear_act_grad stores (act'(u), act(u)) with u = bf16(x W^T + b); mul_bwd_gemm multiplies
+    the dgrad by the stored derivative.  Checked against fp32 math on the same bf16 u, and the
+    derivative's single bf16 rounding is the only difference to the u-storing pair."""
+    torch.manual_seed(6)
+    F, H = 3072, 768
+    x = torch.randn(M, H, device="cuda").bfloat16()
+    w1 = (torch.randn(F, H, device="cuda") * 0.05).bfloat16()
+    b1 = torch.randn(F, device="cuda").bfloat16()
+    g, a = G.linear_act_grad(x, w1, b1, act)
+    u, a_ref = G.linear_gelu(x, w1, b1, act)
+    assert torch.equal(a, a_ref)                       # same activation values bit for bit
+    d_ref = _gelu_grad_ref(u.float(), act)
+    assert (g.float() - d_ref).abs().max().item() < 1e-2          # one bf16 rounding of values <= ~1.13
+    assert rel(g, d_ref) < 4e-3
+    dy = torch.randn(M, H, device="cuda").bfloat16()
+    w2 = (torch.randn(H, F, device="cuda") * 0.05).bfloat16()
+    w2t = w2.t().contiguous()
+    db = torch.zeros(F, device="cuda", dtype=torch.float32)
+    du = G.mul_bwd_gemm(dy, w2t, g, dbias=(db, False))
+    db_u = torch.zeros(F, device="cuda", dtype=torch.float32)
+    du_u = G.gelu_bwd_gemm(dy, w2t, u, dbias=(db_u, False), act=act)
+    ref = (dy.float() @ w2.float()) * d_ref
+    assert rel(du, ref) < 2e-2, rel(du, ref)
+    assert rel(du, du_u) < 1e-2, rel(du, du_u)
+    assert rel(db, ref.sum(0)) < 2e-2
+    assert rel(db, db_u) < 1e-2
+
+
+def test_store_grad_ffn_path_in_model_matches_u_path():
+    """The model's FFN with the derivative stored in the forward (default) gives the same
+    gradients as the pre-activation-storing pair (DTD_GEMM_FFN_STORE_GRAD=0)."""
+    from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
+    from distributed_training_and_deepspeed_amd.models import build_model
+    grads, losses = [], []
+    for on in (False, True):
+        G._FFN_STORE_GRAD[0] = on
+        try:
+            model = build_model("bert-base-cased", dtype=torch.bfloat16, device="cuda", seed=12)
+            ds = SyntheticLMDataset(model.cfg, 16, seq_len=512, seed=3)
+            out = model(ds.input_ids.cuda(), labels=ds.labels.cuda())
+            out.loss.backward()
+            torch.cuda.synchronize()
+            losses.append(out.loss.item())
+            grads.append({n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None})
+        finally:
+            G._FFN_STORE_GRAD[0] = True
+    assert losses[0] == losses[1]                      # identical forward values
+    assert grads[0].keys() == grads[1].keys()
+    for n in grads[0]:
+        g0, g1 = grads[0][n], grads[1][n]
+        err = ((g0 - g1).norm() / (g0.norm() + 1e-12)).item()
+        assert err < 2e-2, (n, err)
