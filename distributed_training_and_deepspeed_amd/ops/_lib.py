@@ -63,7 +63,8 @@ _SIGS = {
     # gemm.hip
     "dtd_gemm_bt_supported": (I, [I, I, I]),
     "dtd_gemm_bt_part_rows": (I, [I]),
-    "dtd_gemm_bt": (I, [I, P, I, P, I, P, I, P, P, I, P, P, I, I, I, P]),
+    "dtd_gemm_bt": (I, [I, P, I, P, I, P, I, P, P, I, P, P, I, I, I, P, P]),
+    "dtd_spin_occupy": (I, [I, ctypes.c_double, P]),
     "dtd_transpose_bf16": (I, [P, P, I, I, P]),
     "dtd_gemm_set_stamps": (I, [P]),
     "dtd_gemm_tn_supported": (I, [I, I, I]),

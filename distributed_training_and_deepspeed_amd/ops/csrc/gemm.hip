@@ -75,7 +75,19 @@ struct GemmArgs {
   float* part;                           // GELU_BWD: [M / 256][N] fp32 column partials (or null)
   int M, N, K, lda, ldb, ldc, ldu;
   unsigned long long* stamps;            // diagnostic builds only (-DDTD_GEMM_STAMPS), else null
+  int* sched;                            // persistent form: dynamic tile queue (see below) or null
 };
+
+// Dynamic tile queue of the persistent form: sched[x] (x = 0..7) is the next unclaimed tile of XCD
+// group x (relative to the group's first tile), sched[8] counts finished workgroups.  A workgroup
+// claims its first two tiles at start; afterwards each tile's epilogue claims the tile after the
+// next one (one device-scope atomic issued when the epilogue starts, its result handed to the
+// other waves through LDS when it ends: the latency hides behind the epilogue and the main loop
+// keeps the static form's registers and schedule), so workgroups that start late -- CUs held
+// by an RCCL kernel on the comm stream, or by a side-stream kernel -- take fewer tiles instead of
+// stretching the launch by their delay.  The last workgroup to finish zeroes the queue for the next
+// launch on the same stream (one queue per stream: ops/gemm.py).
+constexpr int SCHED_DONE = 8;
 
 // In-kernel timing stamps (diagnostic build, scripts/gemm_stamps.py): lane 0 of wave 0 records
 // s_memtime at fixed points of each tile, plus the CU / XCC ids, with plain vector stores.
@@ -645,7 +657,17 @@ __device__ __forceinline__ void tile_of(int t, int ntn, int& m0, int& n0) {
   n0 = (t % ntn) * BN;
 }
 
-template <int EPI>
+// end of a workgroup's claims: the last one to finish zeroes the queue (every claim of this
+// launch has returned by then: each workgroup's final claim precedes its finish count)
+__device__ __forceinline__ void sched_finish(int* q, int nwg, int tid) {
+  if (q == nullptr || tid != 0) return;
+  if (atomicAdd(&q[SCHED_DONE], 1) == nwg - 1) {
+#pragma unroll
+    for (int i = 0; i <= SCHED_DONE; ++i) atomicExch(&q[i], 0);
+  }
+}
+
+template <int EPI, bool DYN>
 __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -658,8 +680,25 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
   const int q = ntiles / 8, r = ntiles % 8;
   const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
   const int end = beg + q + (x < r ? 1 : 0);
-  int t = beg + l;
-  if (t >= end) return;   // more workgroups than tiles in this group (small problems)
+  constexpr bool dyn = DYN;   // g.sched != null (a separate instantiation keeps SGPR pressure)
+  // dynamic queue: iteration j reads the tile of iteration j + 1 from qslot[j & 1]; qslot[2] holds
+  // the first tile
+  __shared__ int qslot[3];
+  int t;
+  if (dyn) {
+    if (tid == 0) {
+      qslot[2] = beg + atomicAdd(&g.sched[x], 1);
+      qslot[0] = beg + atomicAdd(&g.sched[x], 1);
+    }
+    __syncthreads();
+    t = __builtin_amdgcn_readfirstlane(qslot[2]);
+  } else {
+    t = beg + l;
+  }
+  if (t >= end) {   // more workgroups than tiles in this group (small problems) / queue drained
+    if constexpr (DYN) sched_finish(g.sched, nwg, tid);
+    return;
+  }
   int m0, n0;
   tile_of(t, ntn, m0, n0);
   const StageOffs so = stage_offsets(w, lane, g.lda, g.ldb);
@@ -685,7 +724,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
   STAMP_ID(0);
   while (true) {
     STAMP(0, it);
-    const int tn = t + per;
+    const int tn = dyn ? __builtin_amdgcn_readfirstlane(qslot[it & 1]) : t + per;
     const bool has_next = tn < end;
     int m1 = 0, n1 = 0;
     if (has_next) tile_of(tn, ntn, m1, n1);
@@ -805,6 +844,9 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
           for (int k = 0; k < 4; ++k) pk[mi][ni][k] = (bf16)(acc[mi][ni][k] + bv[k]);
       }
     }
+    // dynamic queue: claim the tile after the next one now, publish it when the epilogue ends
+    int claim = 0;
+    if (dyn && has_next && tid == 0) claim = atomicAdd(&g.sched[x], 1);
     if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
     bar();                                                // every wave is done with `img`
     char* img = smem + (buf ^ 1) * TILE_BYTES;            // = the last K-step's buffer
@@ -875,6 +917,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
           *reinterpret_cast<bf16x8*>(g.c + off) = o;
         }
       }
+      if (dyn && rr == 1 && tid == 0) qslot[(it + 1) & 1] = has_next ? beg + claim : end;
       bar();   // the image is consumed before it is rewritten / restaged
     }
     if constexpr (is_gelu_bwd(EPI)) {
@@ -906,6 +949,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
     rsa = rsa1;
     rsb = rsb1;
   }
+  if constexpr (DYN) sched_finish(g.sched, nwg, tid);
 }
 
 // W [rows][cols] -> WT [cols][rows], bf16, 64 x 64 tiles through LDS (padded rows).  Vector form
@@ -994,9 +1038,11 @@ DTD_EXPORT int dtd_gemm_bt_supported(int M, int N, int K) {
 // GELU_BWD column partials: one fp32 row per 256 rows of M
 DTD_EXPORT int dtd_gemm_bt_part_rows(int M) { return M / BM; }
 
+// sched: the stream's dynamic tile queue (9 zero-initialised ints, ops/gemm.py) or null for the
+// static tile order
 DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int ldb, void* c, int ldc, void* c2,
                            const void* u, int ldu, const void* bias, float* part, int M, int N, int K,
-                           hipStream_t s) {
+                           int* sched, hipStream_t s) {
   if (!dtd_gemm_bt_supported(M, N, K)) return (int)hipErrorInvalidValue;
   if ((lda | ldb | ldc) % 8 || (u && ldu % 8)) return (int)hipErrorInvalidValue;
   if (lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
@@ -1004,12 +1050,15 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
   if (is_gelu_fwd(epi) && !c2) return (int)hipErrorInvalidValue;
   if (is_gelu_bwd(epi) && !u) return (int)hipErrorInvalidValue;
   GemmArgs g{(const bf16*)a, (const bf16*)b, (bf16*)c, (bf16*)c2, (const bf16*)u, (const bf16*)bias, part,
-             M, N, K, lda, ldb, ldc, ldu, g_stamps};
+             M, N, K, lda, ldb, ldc, ldu, g_stamps, nullptr};
   const int ntiles = (M / BM) * (N / BN);
   if (gemm_variant() == 1) {
     const int cus = num_cus() / 8 * 8;
     const int nwg = ntiles >= cus ? cus : (ntiles + 7) / 8 * 8;
-#define DTD_GEMM_P(E) hipLaunchKernelGGL(gemm_bt_persistent<E>, dim3(nwg), dim3(512), 0, s, g)
+    g.sched = sched;
+#define DTD_GEMM_P(E)                                                                       \
+  if (sched) hipLaunchKernelGGL((gemm_bt_persistent<E, true>), dim3(nwg), dim3(512), 0, s, g);   \
+  else hipLaunchKernelGGL((gemm_bt_persistent<E, false>), dim3(nwg), dim3(512), 0, s, g)
     switch (epi) {
       case EPI_STORE: DTD_GEMM_P(EPI_STORE); break;
       case EPI_BIAS_GELU: DTD_GEMM_P(EPI_BIAS_GELU); break;
@@ -1042,6 +1091,26 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
     case EPI_MUL_BWD: hipLaunchKernelGGL(gemm_bt_kernel<EPI_MUL_BWD>, grid, dim3(512), 0, s, g); break;
     default: return (int)hipErrorInvalidValue;
   }
+  DTD_LAUNCH_CHECK();
+}
+
+// Diagnostic (scripts/bench_gemm_sched.py): `nwg` workgroups that each hold a whole CU for the
+// persistent GEMM's purposes (96 KiB of LDS: no 128 KiB GEMM workgroup fits beside one) and wait
+// `ticks` of the 100 MHz real-time counter -- a stand-in for an RCCL kernel that occupies CUs on
+// the comm stream while the compute stream launches a GEMM.  Every workgroup exits on its own
+// clock; nothing is written unless the (never true) sink condition holds.
+__global__ void __launch_bounds__(256) spin_occupy_kernel(unsigned long long ticks, int* sink) {
+  __shared__ int hold[24576];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  hold[threadIdx.x] = (int)threadIdx.x;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  __syncthreads();
+  if (sink && hold[threadIdx.x ^ 1] < 0) sink[0] = 1;
+}
+
+DTD_EXPORT int dtd_spin_occupy(int nwg, double us, hipStream_t s) {
+  if (nwg < 1 || nwg > 4096 || !(us >= 0.0) || us > 1e6) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(spin_occupy_kernel, dim3(nwg), dim3(256), 0, s, (unsigned long long)(us * 100.0), nullptr);
   DTD_LAUNCH_CHECK();
 }
 

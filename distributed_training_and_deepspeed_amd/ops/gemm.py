@@ -60,6 +60,14 @@ _FFN_STORE_GRAD = [os.environ.get("DTD_GEMM_FFN_STORE_GRAD", "1") == "1"]
 # (profiles/r2_ab_gemm_oproj.jsonl).  The NT kernel on the transposed o-projection weight (152 vs
 # 164 us in isolation) was neutral end-to-end as well and is not wired in.
 _WGRAD = [os.environ.get("DTD_GEMM_WGRAD", "0") == "1"]
+# Tile order of the persistent kernel: "dynamic" (default) claims tiles from a per-stream atomic
+# queue, so workgroups delayed by CUs that another stream holds (RCCL on the comm stream, the
+# attention-mask generator) take fewer tiles; "static" is the fixed round-robin order (A/B runs).
+_SCHED = [os.environ.get("DTD_GEMM_SCHED", "dynamic")]
+assert _SCHED[0] in ("dynamic", "static"), _SCHED[0]
+_QUEUES: dict = {}
+# epilogues whose dynamic-queue instantiation spills VGPRs in the main loop keep the static order
+_STATIC_EPIS = frozenset({EPI_GELU_TANH_BWD})
 
 
 def enabled() -> bool:
@@ -99,13 +107,32 @@ def supported(M: int, N: int, K: int, *tensors) -> bool:
     return bool(_lib.lib().dtd_gemm_bt_supported(M, N, K))
 
 
+def set_sched(mode: str) -> None:
+    assert mode in ("dynamic", "static"), mode
+    _SCHED[0] = mode
+
+
+def _queue() -> int | None:
+    """The current stream's tile queue (9 int32, zero at rest: the kernel's last workgroup
+    re-zeroes it).  One queue per (device, stream): launches on one stream are ordered, launches
+    on different streams may overlap and must not share counters."""
+    if _SCHED[0] != "dynamic":
+        return None
+    s = torch.cuda.current_stream()   # the stream the kernel is launched on (_lib.stream())
+    key = (s.device_index, s.cuda_stream)
+    q = _QUEUES.get(key)
+    if q is None:
+        q = _QUEUES[key] = torch.zeros(16, dtype=torch.int32, device=torch.device("cuda", s.device_index))
+    return q.data_ptr()
+
+
 def _call(epi, a, b, c, c2=None, u=None, bias=None, part=None):
     M, K = a.shape
     N = b.shape[0]
     assert b.shape[1] == K and c.shape == (M, N), (a.shape, b.shape, c.shape)
     _lib.call("dtd_gemm_bt", epi, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
               _lib.ptr(c2), _lib.ptr(u), u.stride(0) if u is not None else 0, _lib.ptr(bias), _lib.ptr(part),
-              M, N, K, _lib.stream())
+              M, N, K, None if epi in _STATIC_EPIS else _queue(), _lib.stream())
 
 
 def gemm_bt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
