@@ -21,17 +21,18 @@ enum Act : int { kNone = 0, kGeluErf = 1, kGeluTanh = 2, kRelu = 3 };
 // one v_rcp and a handful of FMAs instead of the libm erff's branches and polynomials (the
 // GELU passes are VALU-, not HBM-bound with the libm form).
 __device__ __forceinline__ float phi_cdf(float x, float e) {
-  const float a = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  // t = 1 / (1 + p |x| / sqrt 2): one FMA with an |x| source modifier
+  const float t = __builtin_amdgcn_rcpf(fmaf(fabsf(x), 0.3275911f * 0.70710678118654752f, 1.f));
   const float poly = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
                               0.254829592f);
   const float erfa = 1.f - poly * e;                  // erf(|x| / sqrt 2)
   return 0.5f + 0.5f * copysignf(erfa, x);
 }
-__device__ __forceinline__ float gauss_e(float x) { return __expf(-0.5f * x * x); }
+// exp(-x^2 / 2) as v_exp_f32 (= 2^y) of y = x^2 * (-log2(e) / 2): two multiplies (packable)
+__device__ __forceinline__ float gauss_e(float x) { return __builtin_amdgcn_exp2f((x * x) * -0.72134752044448170f); }
 // tanh(y) = 1 - 2 / (1 + e^{2y}): one v_exp + one v_rcp; saturates correctly at +-inf.
 __device__ __forceinline__ float fast_tanh(float y) {
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * y));
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(y * 2.8853900817779268f));   // e^{2y}
 }
 
 template <int ACT>

@@ -79,9 +79,9 @@ struct GemmArgs {
 };
 
 // Dynamic tile queue of the persistent form: sched[x] (x = 0..7) is the next unclaimed tile of XCD
-// group x (relative to the group's first tile), sched[8] counts finished workgroups.  A workgroup
-// claims its first two tiles at start; afterwards each tile's epilogue claims the tile after the
-// next one (one device-scope atomic issued when the epilogue starts, its result handed to the
+// group x (after the 2 x 32 tiles per group the static order hands out first), sched[8] counts finished
+// workgroups.  A workgroup starts with its first two static tiles; each tile's epilogue claims the
+// tile after the next one (one device-scope atomic issued when the epilogue starts, its result handed to the
 // other waves through LDS when it ends: the latency hides behind the epilogue and the main loop
 // keeps the static form's registers and schedule), so workgroups that start late -- CUs held
 // by an RCCL kernel on the comm stream, or by a side-stream kernel -- take fewer tiles instead of
@@ -123,16 +123,20 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 
 // GELU(erf) and its derivative from one exponential (the formulas of act.hip)
 __device__ __forceinline__ float phi_cdf(float x, float e) {
-  const float a = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  // t = 1 / (1 + p |x| / sqrt 2): one FMA with an |x| source modifier
+  const float t = __builtin_amdgcn_rcpf(fmaf(fabsf(x), 0.3275911f * 0.70710678118654752f, 1.f));
   const float poly = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
                               0.254829592f);
   return 0.5f + 0.5f * copysignf(1.f - poly * e, x);
 }
-__device__ __forceinline__ float gelu(float x) { return x * phi_cdf(x, __expf(-0.5f * x * x)); }
+// exp(-x^2 / 2) as v_exp_f32 (= 2^y) of y = x^2 * (-log2(e) / 2): two multiplies (packable)
+__device__ __forceinline__ float gauss_e(float x) { return __builtin_amdgcn_exp2f((x * x) * -0.72134752044448170f); }
+__device__ __forceinline__ float gelu(float x) { return x * phi_cdf(x, gauss_e(x)); }
 // tanh GELU: 0.5 x (1 + tanh(k (x + 0.044715 x^3))), tanh from one v_exp + one v_rcp (saturates
 // correctly at +-inf) -- the same formula as ops/csrc/act.hip
-__device__ __forceinline__ float tanh_fast(float y) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * y)); }
+__device__ __forceinline__ float tanh_fast(float y) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(y * 2.8853900817779268f));   // e^{2y}
+}
 __device__ __forceinline__ float gelu_tanh(float x) {
   return 0.5f * x * (1.f + tanh_fast(0.7978845608028654f * fmaf(0.044715f * x, x * x, x)));
 }
@@ -167,14 +171,14 @@ __device__ __forceinline__ void epi_act_and_grad(float x, float& a, float& d) {
     a = x * h;
     d = h + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
   } else {
-    const float e = __expf(-0.5f * x * x);
+    const float e = gauss_e(x);
     const float cdf = phi_cdf(x, e);
     a = x * cdf;
     d = fmaf(x * 0.3989422804014327f, e, cdf);
   }
 }
 __device__ __forceinline__ float gelu_grad(float x) {
-  const float e = __expf(-0.5f * x * x);
+  const float e = gauss_e(x);
   return fmaf(x * 0.3989422804014327f, e, phi_cdf(x, e));
 }
 
@@ -681,20 +685,11 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
   const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
   const int end = beg + q + (x < r ? 1 : 0);
   constexpr bool dyn = DYN;   // g.sched != null (a separate instantiation keeps SGPR pressure)
-  // dynamic queue: iteration j reads the tile of iteration j + 1 from qslot[j & 1]; qslot[2] holds
-  // the first tile
-  __shared__ int qslot[3];
-  int t;
-  if (dyn) {
-    if (tid == 0) {
-      qslot[2] = beg + atomicAdd(&g.sched[x], 1);
-      qslot[0] = beg + atomicAdd(&g.sched[x], 1);
-    }
-    __syncthreads();
-    t = __builtin_amdgcn_readfirstlane(qslot[2]);
-  } else {
-    t = beg + l;
-  }
+  // dynamic queue: a workgroup's first two tiles are the static order's (no claims at launch,
+  // where 256 workgroups would contend for 8 counters); queue entry c is tile beg + 2 per + c.
+  // Iteration j >= 1 reads the tile of iteration j + 1 from qslot[j & 1].
+  __shared__ int qslot[2];
+  int t = beg + l;
   if (t >= end) {   // more workgroups than tiles in this group (small problems) / queue drained
     if constexpr (DYN) sched_finish(g.sched, nwg, tid);
     return;
@@ -724,7 +719,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
   STAMP_ID(0);
   while (true) {
     STAMP(0, it);
-    const int tn = dyn ? __builtin_amdgcn_readfirstlane(qslot[it & 1]) : t + per;
+    const int tn = dyn && it > 0 ? __builtin_amdgcn_readfirstlane(qslot[it & 1]) : t + per;
     const bool has_next = tn < end;
     int m1 = 0, n1 = 0;
     if (has_next) tile_of(tn, ntn, m1, n1);
@@ -844,9 +839,6 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
           for (int k = 0; k < 4; ++k) pk[mi][ni][k] = (bf16)(acc[mi][ni][k] + bv[k]);
       }
     }
-    // dynamic queue: claim the tile after the next one now, publish it when the epilogue ends
-    int claim = 0;
-    if (dyn && has_next && tid == 0) claim = atomicAdd(&g.sched[x], 1);
     if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
     bar();                                                // every wave is done with `img`
     char* img = smem + (buf ^ 1) * TILE_BYTES;            // = the last K-step's buffer
@@ -866,8 +858,13 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
     float colsum[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
+    int claim = 0;
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
+      // dynamic queue: claim the tile after the next one when the second round starts (every load
+      // of the epilogue is older, so no counted wait for them waits for the atomic as well);
+      // publish it when the round ends
+      if (dyn && rr == 1 && has_next && tid == 0) claim = atomicAdd(&g.sched[x], 1);
       if (__builtin_amdgcn_readfirstlane(wm) == rr) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
@@ -917,7 +914,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
           *reinterpret_cast<bf16x8*>(g.c + off) = o;
         }
       }
-      if (dyn && rr == 1 && tid == 0) qslot[(it + 1) & 1] = has_next ? beg + claim : end;
+      if (dyn && rr == 1 && tid == 0) qslot[(it + 1) & 1] = has_next ? beg + 2 * per + claim : end;
       bar();   // the image is consumed before it is rewritten / restaged
     }
     if constexpr (is_gelu_bwd(EPI)) {
