@@ -190,9 +190,9 @@ class _MLMHeadFn(torch.autograd.Function):
         x, labels, u, a, t, m, r, logits, lse, stats = ctx.saved_tensors
         head = ctx.head
         c = head.cfg
-        dlogits = Fx.xent_bwd(logits, labels, lse, stats, gloss)
+        # decoder-bias gradient (column sums of dlogits) from the same pass
+        dlogits = Fx.xent_bwd(logits, labels, lse, stats, gloss, dbias=grad_dst(head.decoder_bias))
         del logits
-        Fx.bias_grad(dlogits, *grad_dst(head.decoder_bias))
         grad_done(head.decoder_bias)
         emit_wgrad(head.decoder_weight, dlogits, t)
         dt = dlogits @ head.decoder_weight

@@ -123,6 +123,77 @@ __global__ void __launch_bounds__(256) xent_bwd_kernel(const T* __restrict__ log
   for (int c = body + threadIdx.x; c < V; c += blockDim.x) grad1(c);
 }
 
+// Backward with the decoder-bias gradient fused in (SURVEY.md K8 + the MLM head's bias): the bias
+// gradient is the column sum of dlogits, which the unfused path re-reads from HBM (1.2 GB at
+// bench.py's b256: a 266 us pass).  A block owns a fixed column set -- 4-wide groups c = 4 (t + 512 k),
+// k < XB_GROUPS -- and strides over rows, so every row's dlogits stay in registers for the column
+// sums; each block writes one fp32 partial row ([gridDim.x][V], summed by colsum_finalize).
+// Needs V % 4 == 0 (8-byte row alignment of bf16 rows) and V <= 4 * XB_THREADS * XB_GROUPS.
+constexpr int XB_GROUPS = 16, XB_THREADS = 512;
+__global__ void __launch_bounds__(XB_THREADS) xent_bwd_colsum_kernel(const bf16* __restrict__ logits,
+                                                              const int64_t* __restrict__ labels,
+                                                              const float* __restrict__ lse_row,
+                                                              const float* __restrict__ stats,
+                                                              const float* __restrict__ grad_out,
+                                                              bf16* __restrict__ dlogits, float* __restrict__ part,
+                                                              int rows, int V, int ignore_index) {
+  const int tid = threadIdx.x;
+  const float gs = grad_out[0] / stats[1];
+  float acc[XB_GROUPS][4];
+#pragma unroll
+  for (int k = 0; k < XB_GROUPS; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[k][j] = 0.f;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int64_t y = labels[row];
+    const bf16* z = logits + (size_t)row * V;
+    bf16* dz = dlogits + (size_t)row * V;
+    if (y == ignore_index) {   // zero gradient row (uniform per block)
+#pragma unroll
+      for (int k = 0; k < XB_GROUPS; ++k) {
+        const int c = 4 * (tid + XB_THREADS * k);
+        if (c < V) *reinterpret_cast<bf16x4*>(dz + c) = bf16x4{0, 0, 0, 0};
+      }
+      continue;
+    }
+    const float lse = lse_row[row];
+    const int yr = (int)y - 4 * tid;   // label column relative to this thread's first column
+    // 8 column groups per chunk: loads in flight without holding the whole row in registers
+#pragma unroll
+    for (int kc = 0; kc < XB_GROUPS; kc += 8) {
+      bf16x4 zin[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = 4 * (tid + XB_THREADS * (kc + k));
+        zin[k] = c < V ? *reinterpret_cast<const bf16x4*>(z + c) : bf16x4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = 4 * (tid + XB_THREADS * (kc + k));
+        if (c < V) {
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float p = __expf((float)zin[k][j] - lse);
+            if (4 * XB_THREADS * (kc + k) + j == yr) p -= 1.f;
+            const bf16 d = (bf16)(p * gs);
+            o[j] = d;
+            acc[kc + k][j] += (float)d;   // the bias gradient of the stored (bf16) dlogits
+          }
+          *reinterpret_cast<bf16x4*>(dz + c) = o;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < XB_GROUPS; ++k) {
+    const int c = 4 * (tid + XB_THREADS * k);
+    if (c < V)
+      *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.x * V + c) = f32x4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
+  }
+}
+
 }  // namespace
 
 DTD_EXPORT int dtd_xent_fwd(int dtype, const void* logits, const int64_t* labels, float* loss_row, float* lse_row,
@@ -149,5 +220,23 @@ DTD_EXPORT int dtd_xent_bwd(int dtype, const void* logits, const int64_t* labels
   else
     hipLaunchKernelGGL(xent_bwd_kernel<float>, dim3(rows), dim3(256), 0, s, (const float*)logits, labels, lse_row,
                        stats, grad_out, (float*)dlogits, rows, V, ignore_index);
+  DTD_LAUNCH_CHECK();
+}
+
+// dlogits and the fp32 column partials of dlogits ([parts][V]; colsum_finalize sums them into the
+// decoder-bias gradient).  parts = dtd_xent_bwd_colsum_parts(rows).
+DTD_EXPORT int dtd_xent_bwd_colsum_parts(int rows) { return rows < 256 ? (rows > 0 ? rows : 1) : 256; }
+DTD_EXPORT int dtd_xent_bwd_colsum_supported(int V) { return V > 0 && V % 4 == 0 && V <= 4 * XB_THREADS * XB_GROUPS; }
+DTD_EXPORT int dtd_xent_bwd_colsum(const void* logits, const int64_t* labels, const float* lse_row,
+                                   const float* stats, const float* grad_out, void* dlogits, float* part, int rows,
+                                   int V, int ignore_index, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (!dtd_xent_bwd_colsum_supported(V)) return (int)hipErrorInvalidValue;
+  if (((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(dlogits)) & 7) ||
+      (reinterpret_cast<uintptr_t>(part) & 15))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(xent_bwd_colsum_kernel, dim3(dtd_xent_bwd_colsum_parts(rows)), dim3(XB_THREADS), 0, s,
+                     (const bf16*)logits, labels, lse_row, stats, grad_out, (bf16*)dlogits, part, rows, V,
+                     ignore_index);
   DTD_LAUNCH_CHECK();
 }

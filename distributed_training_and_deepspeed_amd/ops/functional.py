@@ -272,7 +272,10 @@ def xent_fwd(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = IGN
     return stats[0], lse, stats
 
 
-def xent_bwd(logits, labels, lse, stats, grad_out, ignore_index: int = IGNORE_INDEX):
+def xent_bwd(logits, labels, lse, stats, grad_out, ignore_index: int = IGNORE_INDEX, dbias=None):
+    """dlogits of the mean cross-entropy.  ``dbias`` = (dst, acc): also the column sums of dlogits
+    (the bias gradient of the Linear that produced the logits) -- on the kernel path from the same
+    pass (``dtd_xent_bwd_colsum``: no re-read of dlogits) when V % 4 == 0 and V <= 32768."""
     V = logits.shape[-1]
     rows = logits.numel() // V
     labels = labels.reshape(-1)
@@ -282,7 +285,22 @@ def xent_bwd(logits, labels, lse, stats, grad_out, ignore_index: int = IGNORE_IN
         valid = labels != ignore_index
         p[torch.arange(rows), labels.clamp_min(0)] -= 1.0
         p = p * valid[:, None].float() * (grad_out.float() / stats[1])
-        return p.to(logits.dtype).view_as(logits)
+        d = p.to(logits.dtype).view_as(logits)
+        if dbias is not None:
+            bias_grad(d, *dbias)
+        return d
+    if (dbias is not None and logits.dtype == torch.bfloat16 and logits.is_contiguous() and rows > 0
+            and logits.data_ptr() % 8 == 0 and _lib.has("dtd_xent_bwd_colsum")
+            and _lib.lib().dtd_xent_bwd_colsum_supported(V)):
+        d = torch.empty_like(logits)
+        n = _lib.lib().dtd_xent_bwd_colsum_parts(rows)
+        part = torch.empty((n, V), dtype=torch.float32, device=logits.device)
+        gout = grad_out.reshape(1).to(torch.float32).contiguous()
+        _lib.call("dtd_xent_bwd_colsum", logits.data_ptr(), labels.contiguous().to(torch.int64).data_ptr(),
+                  lse.data_ptr(), stats.data_ptr(), gout.data_ptr(), d.data_ptr(), part.data_ptr(), rows, V,
+                  ignore_index, _lib.stream())
+        _finalize(part, n, V, dbias, dbias[1] if isinstance(dbias, tuple) else False)
+        return d
     phase = logits.data_ptr() % 16   # the kernel needs dlogits in the same 16-byte phase
     if phase:
         es = logits.element_size()
@@ -294,6 +312,8 @@ def xent_bwd(logits, labels, lse, stats, grad_out, ignore_index: int = IGNORE_IN
     _lib.call("dtd_xent_bwd", _lib.dt(logits), logits.data_ptr(), labels.contiguous().to(torch.int64).data_ptr(),
               lse.data_ptr(), stats.data_ptr(), gout.data_ptr(), d.data_ptr(), rows, V, ignore_index,
               _lib.stream())
+    if dbias is not None:
+        bias_grad(d, *dbias)
     return d
 
 

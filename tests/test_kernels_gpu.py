@@ -149,6 +149,28 @@ def test_softmax_xent(V, dtype, offset):
     close(res[DEV][3], res["cpu"][3], 2e-2)
 
 
+@pytest.mark.parametrize("V,rows,offset", [(28996, 600, 0), (28996, 37, 0), (1000, 300, 0), (50257, 70, 0),
+                                           (28996, 40, 2)])
+def test_softmax_xent_bwd_fused_bias_grad(V, rows, offset):
+    """xent_bwd(dbias=...) writes dlogits and the column sums of dlogits (the decoder-bias gradient)
+    in one pass on the kernel path (V % 4 == 0, 8-byte aligned); other vocabularies / bases take
+    the two-pass fallback.  dlogits are bit-identical to the unfused kernel; the bias gradient
+    equals an fp32 column sum of the same bf16 dlogits (accumulate and overwrite)."""
+    torch.manual_seed(5)
+    z = (3 * torch.randn(rows * V + offset, device=DEV))[offset:].view(rows, V).bfloat16()
+    lab = torch.randint(0, V, (rows,), device=DEV)
+    lab[::4] = -100
+    gout = torch.tensor(0.9, device=DEV)
+    loss, lse, st = Fx.xent_fwd(z, lab)
+    d_ref = Fx.xent_bwd(z, lab, lse, st, gout)
+    ref = d_ref.float().sum(0)
+    for acc in (False, True):
+        db = torch.full((V,), 0.25, device=DEV)
+        d = Fx.xent_bwd(z, lab, lse, st, gout, dbias=(db, acc))
+        assert torch.equal(d, d_ref)
+        close(db - (0.25 if acc else 0.0), ref, 1e-4)
+
+
 def test_embedding_fwd_bwd():
     torch.manual_seed(3)
     V, h, B, S = 1000, 768, 4, 64
