@@ -41,10 +41,17 @@ def default_backend() -> str:
 
 def init(rank: int | None = None, world_size: int | None = None, backend: str | None = None,
          master_addr: str | None = None, master_port: int | str | None = None, local_rank: int | None = None,
-         timeout_s: float = 1800.0, init_method: str | None = None) -> tuple[int, int]:
+         timeout_s: float = 1800.0, init_method: str | None = None,
+         high_priority: bool | None = None) -> tuple[int, int]:
     """Initialise the default process group (idempotent).  Returns (rank, world_size).
     ``init_method`` (e.g. ``file:///tmp/x/rdzv``) replaces the TCP rendezvous on MASTER_ADDR /
-    MASTER_PORT -- single-host jobs that must not race for a port (tests)."""
+    MASTER_PORT -- single-host jobs that must not race for a port (tests).
+
+    ``high_priority`` (default: env ``DTD_RCCL_HIGH_PRIORITY``, on): RCCL's internal streams are
+    created with high priority, so the dispatcher hands freed CUs to the all-reduce /
+    reduce-scatter kernels that DDP and ZeRO launch during backward before the next compute
+    workgroups -- the collectives overlap the backward instead of queueing behind it.  The
+    persistent GEMMs tolerate the CUs they lose (dynamic tile queue, ops/gemm.py)."""
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     rank = env_rank() if rank is None else rank
@@ -61,6 +68,12 @@ def init(rank: int | None = None, world_size: int | None = None, backend: str | 
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
         kw["device_id"] = torch.device("cuda", local_rank)
+        if high_priority is None:
+            high_priority = os.environ.get("DTD_RCCL_HIGH_PRIORITY", "1") == "1"
+        if high_priority:
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            kw["pg_options"] = opts
     if init_method is not None:
         kw["init_method"] = init_method
     dist.init_process_group(backend=backend, rank=rank, world_size=world_size,

@@ -130,3 +130,16 @@ def test_rccl_bf16_avg_collectives_used_by_ddp_and_zero(rccl_world1):
     clog.all_gather_into_tensor(gat, out, async_op=False)
     torch.cuda.synchronize()
     assert torch.equal(gat, ref)
+
+
+def test_rccl_streams_are_high_priority(rccl_world1):
+    """comm.init creates RCCL's internal streams with high priority (DTD_RCCL_HIGH_PRIORITY
+    default), so backward-overlapped collectives get freed CUs first; a collective still works."""
+    import torch.distributed as dist
+    pg = dist.distributed_c10d._get_default_group()
+    backend = pg._get_backend(torch.device("cuda", 0))
+    assert backend.options.is_high_priority_stream
+    t = torch.full((1024,), 2.0, device="cuda", dtype=torch.bfloat16)
+    dist.all_reduce(t, op=dist.ReduceOp.AVG)
+    torch.cuda.synchronize()
+    assert torch.all(t == 2.0)
