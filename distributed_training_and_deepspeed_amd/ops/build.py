@@ -77,9 +77,24 @@ def _check_kernel_stubs(lib: Path) -> None:
 
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
-    """Compile all kernels for gfx950 and link ``_dtd_kernels.so`` in-tree; return its path."""
+    """Compile all kernels for gfx950 and link ``_dtd_kernels.so`` in-tree; return its path.
+    Concurrent callers (every rank of a job importing a stale library) serialise on a lock file
+    (the objects in ``build/`` are shared) and the library is replaced atomically, so no process
+    loads a half-written one."""
+    import fcntl
     if not force and not needs_build():
         return LIB_PATH
+    with open(HERE / ".build.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if not force and not needs_build():   # another process built it meanwhile
+                return LIB_PATH
+            return _build_locked(force, jobs, verbose)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(force: bool, jobs: int | None, verbose: bool) -> Path:
     hipcc = _hipcc()
     extra = os.environ.get("DTD_HIPCC_FLAGS", "").split()
     srcs = sources()
@@ -90,7 +105,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         print(f"[dtd.build] compiling {len(srcs)} HIP sources for {ARCH} with {jobs} jobs", file=sys.stderr)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, hipcc, extra), srcs))
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+    tmp = LIB_PATH.with_suffix(f".so.tmp{os.getpid()}")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
