@@ -15,6 +15,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -75,6 +77,10 @@ class LayerNorm(nn.Module):
 
 
 # ----------------------------------------------------------------------------- Embeddings
+# DTD_FUSED_EMBED_LN=0 keeps the three-pass embedding forward (A/B runs)
+_FUSED_EMBED_LN = [os.environ.get("DTD_FUSED_EMBED_LN", "1") == "1"]
+
+
 class _EmbedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, mod, *params):
@@ -84,14 +90,22 @@ class _EmbedFn(torch.autograd.Function):
         word = mod.word
         pos = mod.pos
         typ = mod.tok_type
-        z = Fx.embed_fwd(ids, word, pos, typ, S, c.position_offset)
         p = c.hidden_dropout if mod.training else 0.0
         sid = rt.rng.sid(mod.sid)
-        if mod.ln_g is not None:
-            _, x, m, r = Fx.ln_fwd(None, z, mod.ln_g, mod.ln_b, c.ln_eps, 0.0, rt.rng, 0)
+        fused = None
+        if mod.ln_g is not None and _FUSED_EMBED_LN[0]:
+            # gather-sum + LN + dropout in one pass (bit-identical to the three passes below)
+            fused = Fx.embed_ln_fwd(ids, word, pos, typ, S, c.position_offset, mod.ln_g, mod.ln_b, c.ln_eps,
+                                    p, rt.rng, sid)
+        if fused is not None:
+            out, z, m, r = fused
         else:
-            x, m, r = z, None, None
-        out = Fx.dropout(x, p, rt.rng, sid)
+            z = Fx.embed_fwd(ids, word, pos, typ, S, c.position_offset)
+            if mod.ln_g is not None:
+                _, x, m, r = Fx.ln_fwd(None, z, mod.ln_g, mod.ln_b, c.ln_eps, 0.0, rt.rng, 0)
+            else:
+                x, m, r = z, None, None
+            out = Fx.dropout(x, p, rt.rng, sid)
         ctx.save_for_backward(ids, z, m, r)
         ctx.mod, ctx.p, ctx.sid, ctx.rng = mod, p, sid, rt.rng
         return out.view(B, S, h)

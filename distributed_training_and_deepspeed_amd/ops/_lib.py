@@ -51,6 +51,7 @@ _SIGS = {
     "dtd_embed_word_bwd": (I, [I, I, P, P, P, P, I, I, I, I, P]),
     "dtd_embed_pos_bwd": (I, [I, I, P, P, I, I, I, I, I, P]),
     "dtd_dropout": (I, [I, P, P, P, SZ, F, P, U32, P]),
+    "dtd_embed_ln_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, F, F, P, U32, P]),
     # adam.hip
     "dtd_adam_step": (I, [P, P, P, P, I, P, SZ, P, I, P]),
     "dtd_scale_cast": (I, [P, I, P, I, SZ, F, P, P]),

@@ -369,6 +369,84 @@ void dispatch(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream
   else hipLaunchKernelGGL((ln_bwd_block<T>), dim3(nblocks_bwd), dim3(256), 0, s, *b);
 }
 
+// Embedding forward in one pass (SURVEY.md K7 + K4 + K6; HF BertEmbeddings): z = word[id] +
+// pos[s + offset] + type[type_id] (fp32 sum, stored as bf16 for the LayerNorm backward), x =
+// LN(z) of the stored bf16 z, out = dropout(bf16(x)).  Bit-identical to dtd_embed_fwd ->
+// dtd_ln_fwd (r = z) -> dtd_dropout: the same lane / column map and row reduction as ln_fwd_wave
+// and the same keep-bit law and element index as dropout_kernel, with the two intermediate
+// [rows, h] round trips through HBM (z re-read, x written and re-read) gone.
+struct EmbLnArgs {
+  const int64_t* ids; const int64_t* type_ids; const void* word; const void* pos; const void* type;
+  const void* gamma; const void* beta; void* z; void* out; float* mean; float* rstd;
+  int rows, h, seq, pos_offset; float eps, p; const uint64_t* rng; uint32_t stream_id;
+};
+
+template <int VEC, int ITERS, int LPR>
+__global__ void __launch_bounds__(256) emb_ln_fwd_wave(EmbLnArgs a) {
+  using T = bf16;
+  constexpr int NPL = VEC * ITERS, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int row0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool valid = row0 < a.rows;
+  const int row = valid ? row0 : a.rows - 1;     // keep every lane of the wave in the shuffles
+  const int h = a.h;
+  const size_t base = (size_t)row * h;
+  const int64_t id = a.ids[row];
+  const int64_t ty = a.type_ids ? a.type_ids[row] : 0;
+  const T* w = (const T*)a.word + (size_t)id * h;
+  const T* ps = a.pos ? (const T*)a.pos + (size_t)((row % a.seq) + a.pos_offset) * h : nullptr;
+  const T* tp = a.type ? (const T*)a.type + (size_t)ty * h : nullptr;
+  float z[NPL];
+#pragma unroll
+  for (int c = 0; c < ITERS; ++c) {
+    const int col = (c * LPR + sub) * VEC;
+    float t[VEC], u[VEC];
+    vload<T, VEC>(w + col, t);
+    if (ps) {
+      vload<T, VEC>(ps + col, u);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) t[j] += u[j];
+    }
+    if (tp) {
+      vload<T, VEC>(tp + col, u);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) t[j] += u[j];
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) t[j] = (float)(T)t[j];   // the stored bf16 z feeds the LN
+    if (valid) vstore_nt<T, VEC>((T*)a.z + base + col, t);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) z[c * VEC + j] = t[j];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) s += z[i];
+  const float mu = row_sum<LPR>(s) / h;
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) { float d = z[i] - mu; v += d * d; }
+  const float rs = rsqrtf(row_sum<LPR>(v) / h + a.eps);
+  if (!valid) return;
+  if (sub == 0) { a.mean[row] = mu; a.rstd[row] = rs; }
+  const bool has_drop = a.p > 0.f;
+  DropoutRng g(a.rng, a.stream_id);
+  const uint32_t thr = keep_threshold(a.p);
+  const float scale = has_drop ? 1.f / (1.f - a.p) : 1.f;
+#pragma unroll
+  for (int c = 0; c < ITERS; ++c) {
+    const int col = (c * LPR + sub) * VEC;
+    float gm[VEC], bt[VEC], o[VEC];
+    vload<T, VEC>((const T*)a.gamma + col, gm);
+    vload<T, VEC>((const T*)a.beta + col, bt);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      o[j] = (float)(T)((z[c * VEC + j] - mu) * rs * gm[j] + bt[j]);   // x, rounded as stored
+      if (has_drop) o[j] *= drop_factor(g, base + col + j, thr, scale);
+    }
+    vstore_nt<T, VEC>((T*)a.out + base + col, o);
+  }
+}
+
 }  // namespace
 
 // Number of partial rows the backward writes (callers size part_* as [n, h] fp32).
@@ -405,5 +483,26 @@ DTD_EXPORT int dtd_ln_bwd(int dtype, const void* dout, const void* dout2, const 
   const int nb = dtd_ln_bwd_num_partials(rows, h);
   if (dtype == kBF16) dispatch<bf16>(nullptr, &a, nb, s);
   else dispatch<float>(nullptr, &a, nb, s);
+  DTD_LAUNCH_CHECK();
+}
+
+// Fused embedding gather-sum + LayerNorm + dropout (bf16, h = 768 or 1024; else -1: the caller
+// takes dtd_embed_fwd -> dtd_ln_fwd -> dtd_dropout).  z [rows, h] (LN input, for the backward),
+// out [rows, h], mean / rstd [rows].
+DTD_EXPORT int dtd_embed_ln_fwd(const int64_t* ids, const int64_t* type_ids, const void* word, const void* pos,
+                                const void* type, const void* gamma, const void* beta, void* z, void* out, float* mean,
+                                float* rstd, int rows, int h, int seq, int pos_offset, float eps, float p,
+                                const uint64_t* rng, uint32_t stream_id, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (seq <= 0 || rng == nullptr) return (int)hipErrorInvalidValue;   // rng is read even at p = 0
+  EmbLnArgs a{ids, type_ids, word, pos, type, gamma, beta, z, out, mean, rstd, rows, h, seq, pos_offset, eps, p,
+              rng, stream_id};
+  if (h == 768) {
+    hipLaunchKernelGGL((emb_ln_fwd_wave<8, 3, 32>), dim3((rows + 7) / 8), dim3(256), 0, s, a);
+  } else if (h == 1024) {
+    hipLaunchKernelGGL((emb_ln_fwd_wave<8, 2, 64>), dim3((rows + 3) / 4), dim3(256), 0, s, a);
+  } else {
+    return -1;
+  }
   DTD_LAUNCH_CHECK();
 }

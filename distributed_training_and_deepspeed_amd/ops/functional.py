@@ -342,6 +342,32 @@ def embed_fwd(ids: torch.Tensor, word: torch.Tensor, pos: torch.Tensor | None, t
     return out
 
 
+def embed_ln_fwd(ids, word, pos, type_, seq: int, pos_offset: int, gamma, beta, eps: float, p: float,
+                 rng: RngState, sid: int, type_ids=None):
+    """Embedding gather-sum + LayerNorm + dropout in one kernel: returns (out, z, mean, rstd), the
+    same values as ``embed_fwd`` -> ``ln_fwd(None, z, ...)`` -> ``dropout`` (z = the LN input the
+    backward needs), or None when the fused kernel does not cover the case (CPU, fp32, h other
+    than 768 / 1024): the caller then runs the three passes."""
+    h = word.shape[1]
+    if (not _on_gpu(word) or word.dtype != torch.bfloat16 or h not in (768, 1024) or gamma is None
+            or not _lib.has("dtd_embed_ln_fwd")
+            or any(t is not None and (t.dtype != torch.bfloat16 or not t.is_contiguous())
+                   for t in (word, pos, type_, gamma, beta))):
+        return None
+    rows = ids.numel()
+    z = torch.empty((rows, h), dtype=word.dtype, device=word.device)
+    out = torch.empty_like(z)
+    mean = torch.empty(rows, dtype=torch.float32, device=word.device)
+    rstd = torch.empty_like(mean)
+    ids_c = ids.reshape(-1).contiguous().to(torch.int64)
+    tids = type_ids.reshape(-1).contiguous().to(torch.int64) if type_ids is not None else None
+    _lib.call("dtd_embed_ln_fwd", ids_c.data_ptr(), _lib.ptr(tids), word.data_ptr(), _lib.ptr(pos), _lib.ptr(type_),
+              gamma.data_ptr(), beta.data_ptr(), z.data_ptr(), out.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+              rows, h, seq, pos_offset, float(eps), float(p), rng.state.data_ptr(), sid,
+              _lib.stream())
+    return out, z, mean, rstd
+
+
 def embed_word_bwd(ids: torch.Tensor, dz: torch.Tensor, grad: torch.Tensor, acc: bool, padding_idx: int = -1):
     flat = ids.reshape(-1)
     h = grad.shape[1]

@@ -281,3 +281,31 @@ def test_row_softmax_fwd_bwd(n, dtype):
     dx = Fx.softmax_bwd(y, dy.to(DEV))
     rdx = ref * (dy.float() - (ref * dy.float()).sum(-1, keepdim=True))
     close(dx, rdx, 3e-2 if dtype == torch.bfloat16 else 1e-4)
+
+
+@pytest.mark.parametrize("h,rows,seq,offset,p", [(768, 131 * 3, 131, 0, 0.1), (768, 512 * 4, 512, 0, 0.0),
+                                                 (1024, 67 * 3, 67, 2, 0.1)])
+def test_embed_ln_dropout_fused_bit_identical(h, rows, seq, offset, p):
+    """embed_ln_fwd (one kernel) == embed_fwd -> ln_fwd -> dropout: z (the LN input kept for the
+    backward) and mean bit for bit, rstd to the last fp32 bits (the two kernels' rsqrt codegen may
+    differ by an ulp), the dropped-out output to one bf16 rounding at most, with identical keep
+    bits; rows not a multiple of the 8 rows per block."""
+    from distributed_training_and_deepspeed_amd.ops.rng import RngState
+    torch.manual_seed(7)
+    V = 1000
+    word = (torch.randn(V, h, device=DEV) * 0.5).bfloat16()
+    pos = (torch.randn(seq + offset, h, device=DEV) * 0.1).bfloat16()
+    typ = (torch.randn(2, h, device=DEV) * 0.1).bfloat16()
+    g = (1 + 0.1 * torch.randn(h, device=DEV)).bfloat16()
+    b = (0.1 * torch.randn(h, device=DEV)).bfloat16()
+    ids = torch.randint(0, V, (rows // seq, seq), device=DEV)
+    rng = RngState(1234, device=DEV)
+    out, z, m, r = Fx.embed_ln_fwd(ids, word, pos, typ, seq, offset, g, b, 1e-12, p, rng, 5)
+    z_ref = Fx.embed_fwd(ids, word, pos, typ, seq, offset)
+    _, x_ref, m_ref, r_ref = Fx.ln_fwd(None, z_ref, g, b, 1e-12, 0.0, rng, 0)
+    out_ref = Fx.dropout(x_ref, p, rng, 5)
+    assert torch.equal(z, z_ref)
+    assert torch.equal(m, m_ref)
+    assert ((r - r_ref).abs() <= 4e-7 * r_ref.abs()).all()
+    assert torch.equal(out == 0, out_ref == 0)                       # the same dropped elements
+    assert ((out.float() - out_ref.float()).abs() <= 8e-3 * out_ref.float().abs() + 1e-6).all()
