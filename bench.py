@@ -62,6 +62,9 @@ def parse():
                     help="sparse MLM head rows: a fixed capacity (mean + 8 sigma of the 15%% law, rounded "
                          "to 256; constant GEMM shapes, no per-step host sync; overflow raises) or the exact "
                          "labelled-row count per batch")
+    ap.add_argument("--opt-overlap", default=os.environ.get("DTD_OPT_OVERLAP", "on"), choices=["on", "off"],
+                    help="DDP: the Adam update runs stage by stage on a side stream and the next forward "
+                         "waits per stage (FusedAdam.overlap_with_forward; bit-identical results)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
     return ap.parse_args()
@@ -144,6 +147,10 @@ def main():
         from distributed_training_and_deepspeed_amd.utils.graphs import mlm_capacity
         model.rt.mlm_capacity = -(-mlm_capacity(B * S) // 256) * 256
         model.rt.mlm_overflow = torch.zeros((), dtype=torch.bool, device=device)
+    opt_overlap = (not zero and cuda and args.graph != "on" and args.opt_overlap == "on"
+                   and hasattr(opt, "overlap_with_forward") and hasattr(model, "zero3_units"))
+    if opt_overlap:
+        opt.overlap_with_forward(model.zero3_units())
     graphed = None
     if args.graph == "on" and cuda and not zero:
         # one hipGraph replay per step (host-launch-bound small batches); static-size MLM head
@@ -217,6 +224,7 @@ def main():
                 "tuned_gemms": tuned,
                 "hip_graph": graphed is not None,
                 "async_wgrad": args.async_wgrad == "on",
+                "opt_overlap": opt_overlap,
                 "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if cuda else None,
             },
             "loss_first": round(first_loss, 4),

@@ -80,6 +80,7 @@ class FusedAdam(torch.optim.Optimizer):
         self.hp = torch.zeros(8, dtype=torch.float32, device=dev)
         self._hp_host = None
         self.step_count = 0
+        self._chunks = None
         self._push_hparams()
         return self
 
@@ -107,6 +108,7 @@ class FusedAdam(torch.optim.Optimizer):
         self.hp = torch.zeros(8, dtype=torch.float32, device=dev)
         self._hp_host = None
         self.step_count = 0
+        self._chunks = None
         self._push_hparams()
 
     @staticmethod
@@ -139,6 +141,7 @@ class FusedAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        self.synchronize()   # staged updates of the previous step: hp / gradients are rewritten below
         if self.gbuf is not None:  # gradients assigned to p.grad by hand (not via autograd)
             for p in self._params:
                 g = p.grad
@@ -160,7 +163,9 @@ class FusedAdam(torch.optim.Optimizer):
             norm = sq.sqrt()
             self.hp[6:7].copy_(torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0).reshape(1))
         n = self.master.numel()
-        if self.master.is_cuda:
+        if self.master.is_cuda and self._chunks is not None:
+            self._step_staged()
+        elif self.master.is_cuda:
             _lib.call("dtd_adam_step", self.master.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
                       self.grad_flat.data_ptr(), _lib.dt(self.grad_flat), _lib.ptr(self.lowp), n,
                       self.hp.data_ptr(), self.mode, _lib.stream())
@@ -175,6 +180,94 @@ class FusedAdam(torch.optim.Optimizer):
             self.gbuf.reset()
         return loss
 
+    # ------------------------------------------------------------------ overlap with forward
+    def overlap_with_forward(self, stages) -> None:
+        """Let the next forward start while later stages' parameters are still being updated.
+        ``stages``: the model's modules in forward order (e.g. ``model.zero3_units()``).
+        step() then runs the same Adam kernel stage by stage on a side stream and records one
+        event per stage; a forward pre-hook on each stage makes the compute stream wait for that
+        stage's parameters only, so the HBM-bound update of the later stages runs under the first
+        stages' MFMA-bound GEMMs instead of before them.  Elements no stage owns (padding, params
+        registered elsewhere) are updated first and waited for by the first stage; a post-hook on
+        the last stage waits for every chunk (the next backward overwrites the gradients the
+        kernel reads).  Per element the math is the single launch's: results are bit-identical."""
+        if not self.master.is_cuda or self._chunks is not None:
+            return
+        base = self.param_flat
+        st = base.untyped_storage().data_ptr()
+        n = self.master.numel()
+        spans = []   # (start, end, stage index)
+        for k, m in enumerate(stages):
+            for p in m.parameters():
+                if p.untyped_storage().data_ptr() != st or not p.requires_grad:
+                    continue
+                off = p.storage_offset() - base.storage_offset()
+                if 0 <= off and off + p.numel() <= n:
+                    spans.append((off, off + p.numel(), k))
+        spans.sort()
+        chunks = {k: [] for k in range(-1, len(stages))}   # -1: elements no stage owns
+        pos = 0
+        for a, b, k in spans:
+            a = max(a, pos)
+            if a >= b:
+                continue   # shared by an earlier stage (tied parameters)
+            if a > pos:
+                chunks[-1].append((pos, a))
+            chunks[k].append((a, b))
+            pos = b
+        if pos < n:
+            chunks[-1].append((pos, n))
+        # merge adjacent ranges of one stage
+        for k, rs in chunks.items():
+            merged = []
+            for a, b in sorted(rs):
+                if merged and merged[-1][1] == a:
+                    merged[-1] = (merged[-1][0], b)
+                else:
+                    merged.append((a, b))
+            chunks[k] = merged
+        self._chunks = [chunks[k] for k in range(-1, len(stages))]
+        self._side = torch.cuda.Stream(self.master.device)
+        self._events = [None] * len(self._chunks)
+        self._hooks = []
+        last = len(stages) - 1
+        for k, m in enumerate(stages):
+            waits = (0, k + 1) if k == 0 else (k + 1,)
+            self._hooks.append(m.register_forward_pre_hook(
+                lambda mod, inp, w=waits: self._wait(w)))
+        self._hooks.append(stages[last].register_forward_hook(
+            lambda mod, inp, out: self.synchronize()))
+
+    def _wait(self, idx) -> None:
+        cur = torch.cuda.current_stream(self.master.device)
+        for i in idx:
+            ev = self._events[i]
+            if ev is not None:
+                cur.wait_event(ev)
+                self._events[i] = None
+
+    def synchronize(self) -> None:
+        """Make the current stream wait for every staged update still pending."""
+        if self._chunks is not None:
+            self._wait(range(len(self._events)))
+
+    def _step_staged(self) -> None:
+        self.synchronize()   # a previous step's chunks no forward waited for
+        side = self._side
+        side.wait_stream(torch.cuda.current_stream(self.master.device))
+        es, gs = 4, self.grad_flat.element_size()
+        lp = self.lowp
+        with torch.cuda.stream(side):
+            for i, rs in enumerate(self._chunks):
+                for a, b in rs:
+                    _lib.call("dtd_adam_step", self.master.data_ptr() + a * es, self.exp_avg.data_ptr() + a * es,
+                              self.exp_avg_sq.data_ptr() + a * es, self.grad_flat.data_ptr() + a * gs,
+                              _lib.dt(self.grad_flat), None if lp is None else lp.data_ptr() + a * lp.element_size(),
+                              b - a, self.hp.data_ptr(), self.mode, side.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                self._events[i] = ev
+
     def zero_grad(self, set_to_none: bool = True):
         if self.gbuf is not None:
             self.gbuf.reset()
@@ -182,6 +275,7 @@ class FusedAdam(torch.optim.Optimizer):
             p.grad = None
 
     def state_dict(self):
+        self.synchronize()
         # under hipGraph replay only the device copy of the step count advances
         step = int(self.hp[5].item()) if self.hp.is_cuda else self.step_count
         return {"step": step, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
@@ -189,6 +283,7 @@ class FusedAdam(torch.optim.Optimizer):
                                                          for g in self.param_groups]}
 
     def load_state_dict(self, sd):
+        self.synchronize()
         self.step_count = int(sd["step"])
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])

@@ -34,6 +34,8 @@ def _rank() -> int:
 
 def save_checkpoint(path: str, model: torch.nn.Module, optimizer=None, step: int = 0, extra: dict | None = None) -> str:
     """Rank 0 writes ``path`` (a file); all ranks return after the write completed."""
+    if optimizer is not None and hasattr(optimizer, "synchronize"):
+        optimizer.synchronize()   # a staged update (overlap_with_forward) may still be writing weights
     if _rank() == 0:
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         rt = getattr(model, "rt", None)
@@ -55,6 +57,8 @@ def save_checkpoint(path: str, model: torch.nn.Module, optimizer=None, step: int
 def load_checkpoint(path: str, model: torch.nn.Module, optimizer=None) -> dict:
     """Restore module (+ optimizer, dropout RNG); returns {'step', 'extra'}."""
     state = torch.load(path, map_location="cpu", weights_only=True)
+    if optimizer is not None and hasattr(optimizer, "synchronize"):
+        optimizer.synchronize()
     model.load_state_dict(state["module"])
     if optimizer is not None and state.get("optimizer") is not None:
         optimizer.load_state_dict(state["optimizer"])
