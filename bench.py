@@ -150,7 +150,7 @@ def main():
     opt_overlap = (not zero and cuda and args.graph != "on" and args.opt_overlap == "on"
                    and hasattr(opt, "overlap_with_forward") and hasattr(model, "zero3_units"))
     if opt_overlap:
-        opt.overlap_with_forward(model.zero3_units())
+        opt.overlap_with_forward(model.zero3_units(), root=model)
     graphed = None
     if args.graph == "on" and cuda and not zero:
         # one hipGraph replay per step (host-launch-bound small batches); static-size MLM head

@@ -93,7 +93,7 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
 
     if graphed is None and cuda and hasattr(model, "zero3_units"):
         # eager steps: the Adam update of later stages overlaps the next forward (bit-identical)
-        optimizer.overlap_with_forward(model.zero3_units())
+        optimizer.overlap_with_forward(model.zero3_units(), root=model)
     timer = StepTimer(batch_size * opts.seq_len, world_size)
     start = time.time()
     n = 0  # timed steps (graph warm-up steps trained before the clock started)

@@ -63,5 +63,5 @@ class BertForMaskedLM(nn.Module):
         if labels is not None:
             out.loss = self.head(x, labels)
         if labels is None or return_logits:
-            out.logits = self.head.logits(x)
+            out.logits = self.head(x)   # module call: ZeRO-3 / staged-optimizer hooks fire
         return out

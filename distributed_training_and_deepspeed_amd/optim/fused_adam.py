@@ -181,7 +181,7 @@ class FusedAdam(torch.optim.Optimizer):
         return loss
 
     # ------------------------------------------------------------------ overlap with forward
-    def overlap_with_forward(self, stages) -> None:
+    def overlap_with_forward(self, stages, root=None) -> None:
         """Let the next forward start while later stages' parameters are still being updated.
         ``stages``: the model's modules in forward order (e.g. ``model.zero3_units()``).
         step() then runs the same Adam kernel stage by stage on a side stream and records one
@@ -189,8 +189,8 @@ class FusedAdam(torch.optim.Optimizer):
         stage's parameters only, so the HBM-bound update of the later stages runs under the first
         stages' MFMA-bound GEMMs instead of before them.  Elements no stage owns (padding, params
         registered elsewhere) are updated first and waited for by the first stage; a post-hook on
-        the last stage waits for every chunk (the next backward overwrites the gradients the
-        kernel reads).  Per element the math is the single launch's: results are bit-identical."""
+        ``root`` (the whole model; default: the last stage) waits for every chunk before anything
+        after the forward runs (the next backward overwrites the gradients the kernel reads).  Per element the math is the single launch's: results are bit-identical."""
         if not self.master.is_cuda or self._chunks is not None:
             return
         base = self.param_flat
@@ -235,7 +235,7 @@ class FusedAdam(torch.optim.Optimizer):
             waits = (0, k + 1) if k == 0 else (k + 1,)
             self._hooks.append(m.register_forward_pre_hook(
                 lambda mod, inp, w=waits: self._wait(w)))
-        self._hooks.append(stages[last].register_forward_hook(
+        self._hooks.append((root if root is not None else stages[last]).register_forward_hook(
             lambda mod, inp, out: self.synchronize()))
 
     def _wait(self, idx) -> None:

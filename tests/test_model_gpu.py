@@ -100,7 +100,7 @@ def test_staged_adam_overlapped_with_forward_is_bit_identical():
         ddp = DistributedDataParallel(model)
         opt = hf_adamw(ddp.parameters(), lr=1e-3)
         if overlap:
-            opt.overlap_with_forward(model.zero3_units())
+            opt.overlap_with_forward(model.zero3_units(), root=model)
             assert opt._chunks is not None and sum(len(c) for c in opt._chunks) >= len(model.zero3_units())
         ds = SyntheticLMDataset(model.cfg, 8, seq_len=128, seed=0)
         ids, lab = ds.input_ids.view(4, 2, 128).cuda(), ds.labels.view(4, 2, 128).cuda()
