@@ -183,6 +183,12 @@ class Embeddings(nn.Module):
 
 
 # ----------------------------------------------------------------------------- MLM head
+# DTD_FUSED_XENT=1: the training forward computes loss, dlogits and the decoder-bias gradient in
+# one pass (Fx.xent_fwd_train).  Off by default: -0.6 % end-to-end same box -- its per-row block
+# reductions serialise the column-owning blocks (profiles/r2_ab_fused_xent_experiment.jsonl)
+_FUSED_XENT = [os.environ.get("DTD_FUSED_XENT", "0") == "1"]
+
+
 class _MLMHeadFn(torch.autograd.Function):
     """x [T,h] rows (already gathered for the sparse head) -> loss (mean over valid labels)."""
 
@@ -194,19 +200,37 @@ class _MLMHeadFn(torch.autograd.Function):
         ctx.rng = head.rt.rng
         _, t, m, r = Fx.ln_fwd(None, a, head.ln_g, head.ln_b, c.ln_eps, 0.0, ctx.rng, 0)
         logits = F.linear(t, head.decoder_weight, head.decoder_bias)
-        loss, lse, stats = Fx.xent_fwd(logits, labels)
-        ctx.save_for_backward(x, labels, u, a, t, m, r, logits, lse, stats)
+        fused = Fx.xent_fwd_train(logits, labels) if any(ctx.needs_input_grad) and _FUSED_XENT[0] else None
+        if fused is not None:
+            # loss, dlogits and the decoder-bias gradient in one pass over the logits (for a loss
+            # gradient of 1; the backward rescales otherwise): the logits are not kept
+            loss, _, _, dlogits, dbias = fused
+            ctx.save_for_backward(x, labels, u, a, t, m, r, dlogits, dbias)
+        else:
+            loss, lse, stats = Fx.xent_fwd(logits, labels)
+            ctx.save_for_backward(x, labels, u, a, t, m, r, logits, lse, stats)
+        ctx.fused = fused is not None
         ctx.head = head
         return loss
 
     @staticmethod
     def backward(ctx, gloss):
-        x, labels, u, a, t, m, r, logits, lse, stats = ctx.saved_tensors
         head = ctx.head
         c = head.cfg
-        # decoder-bias gradient (column sums of dlogits) from the same pass
-        dlogits = Fx.xent_bwd(logits, labels, lse, stats, gloss, dbias=grad_dst(head.decoder_bias))
-        del logits
+        if ctx.fused:
+            x, labels, u, a, t, m, r, dlogits, dbias = ctx.saved_tensors
+            Fx.xent_grad_scale_(dlogits, gloss)
+            dst, acc = grad_dst(head.decoder_bias)
+            g = dbias * gloss.reshape(1).float()
+            if acc:
+                dst.add_(g.to(dst.dtype))
+            else:
+                dst.copy_(g)
+        else:
+            x, labels, u, a, t, m, r, logits, lse, stats = ctx.saved_tensors
+            # decoder-bias gradient (column sums of dlogits) from the same pass
+            dlogits = Fx.xent_bwd(logits, labels, lse, stats, gloss, dbias=grad_dst(head.decoder_bias))
+            del logits
         grad_done(head.decoder_bias)
         emit_wgrad(head.decoder_weight, dlogits, t)
         dt = dlogits @ head.decoder_weight

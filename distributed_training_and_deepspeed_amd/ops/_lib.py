@@ -46,6 +46,8 @@ _SIGS = {
     "dtd_xent_bwd_colsum_parts": (I, [I]),
     "dtd_xent_bwd_colsum_supported": (I, [I]),
     "dtd_xent_bwd_colsum": (I, [P, P, P, P, P, P, P, I, I, I, P]),
+    "dtd_xent_fwd_train": (I, [P, P, P, P, P, P, P, I, I, I, P]),
+    "dtd_xent_grad_scale": (I, [P, SZ, P, P]),
     # embed.hip
     "dtd_embed_fwd": (I, [I, P, P, P, P, P, P, I, I, I, I, P]),
     "dtd_embed_word_bwd": (I, [I, I, P, P, P, P, I, I, I, I, P]),

@@ -83,14 +83,14 @@ __global__ void __launch_bounds__(1024) xent_reduce_kernel(const float* __restri
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       y[k] = labels[r + k * n];
-      l[k] = loss_row[r + k * n];
+      l[k] = loss_row ? loss_row[r + k * n] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (y[k] != ignore_index) { s += l[k]; c += 1.f; }
   }
   for (; r < rows; r += n) {
-    if (labels[r] != ignore_index) { s += loss_row[r]; c += 1.f; }
+    if (labels[r] != ignore_index) { s += loss_row ? loss_row[r] : 0.f; c += 1.f; }
   }
   s = block_sum(s, sh);
   c = block_sum(c, sh);
@@ -146,15 +146,22 @@ __global__ void __launch_bounds__(256) xent_bwd_kernel(const T* __restrict__ log
 // sums; each block writes one fp32 partial row ([gridDim.x][V], summed by colsum_finalize).
 // Needs V % 4 == 0 (8-byte row alignment of bf16 rows) and V <= 4 * XB_THREADS * XB_GROUPS.
 constexpr int XB_GROUPS = 16, XB_THREADS = 512;
+// FWD = true (training forward, dtd_xent_fwd_train): the block also computes each row's
+// log-sum-exp from the row it holds in registers (two block reductions per row) and writes
+// lse_row / loss_row, with the gradient scale 1 / count (grad_out = 1; the backward rescales
+// when the loss gradient is not 1) -- the logits are read once for the loss and the gradient.
+template <bool FWD>
 __global__ void __launch_bounds__(XB_THREADS) xent_bwd_colsum_kernel(const bf16* __restrict__ logits,
                                                               const int64_t* __restrict__ labels,
-                                                              const float* __restrict__ lse_row,
+                                                              float* __restrict__ lse_row,
                                                               const float* __restrict__ stats,
                                                               const float* __restrict__ grad_out,
                                                               bf16* __restrict__ dlogits, float* __restrict__ part,
+                                                              float* __restrict__ loss_row,
                                                               int rows, int V, int ignore_index) {
+  __shared__ float sh[XB_THREADS / 64];
   const int tid = threadIdx.x;
-  const float gs = grad_out[0] / stats[1];
+  const float gs = (FWD ? 1.f : grad_out[0]) / stats[1];
   float acc[XB_GROUPS][4];
 #pragma unroll
   for (int k = 0; k < XB_GROUPS; ++k)
@@ -170,9 +177,37 @@ __global__ void __launch_bounds__(XB_THREADS) xent_bwd_colsum_kernel(const bf16*
         const int c = 4 * (tid + XB_THREADS * k);
         if (c < V) *reinterpret_cast<bf16x4*>(dz + c) = bf16x4{0, 0, 0, 0};
       }
+      if (FWD && tid == 0) { lse_row[row] = 0.f; loss_row[row] = 0.f; }
       continue;
     }
-    const float lse = lse_row[row];
+    float lse;
+    if constexpr (FWD) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < XB_GROUPS; ++k) {
+        const int c = 4 * (tid + XB_THREADS * k);
+        if (c < V) {
+          const bf16x4 q = *reinterpret_cast<const bf16x4*>(z + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mx = fmaxf(mx, (float)q[j]);
+        }
+      }
+      const float M = block_max(mx, sh);
+      float se = 0.f;
+#pragma unroll
+      for (int k = 0; k < XB_GROUPS; ++k) {
+        const int c = 4 * (tid + XB_THREADS * k);
+        if (c < V) {
+          const bf16x4 q = *reinterpret_cast<const bf16x4*>(z + c);   // L1/L2 hit: read just above
+#pragma unroll
+          for (int j = 0; j < 4; ++j) se += __expf((float)q[j] - M);
+        }
+      }
+      lse = M + __logf(block_sum(se, sh));
+      if (tid == 0) { lse_row[row] = lse; loss_row[row] = lse - (float)z[y]; }
+    } else {
+      lse = lse_row[row];
+    }
     const int yr = (int)y - 4 * tid;   // label column relative to this thread's first column
     // 8 column groups per chunk: loads in flight without holding the whole row in registers
 #pragma unroll
@@ -251,8 +286,56 @@ DTD_EXPORT int dtd_xent_bwd_colsum(const void* logits, const int64_t* labels, co
   if (((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(dlogits)) & 7) ||
       (reinterpret_cast<uintptr_t>(part) & 15))
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(xent_bwd_colsum_kernel, dim3(dtd_xent_bwd_colsum_parts(rows)), dim3(XB_THREADS), 0, s,
-                     (const bf16*)logits, labels, lse_row, stats, grad_out, (bf16*)dlogits, part, rows, V,
-                     ignore_index);
+  hipLaunchKernelGGL(xent_bwd_colsum_kernel<false>, dim3(dtd_xent_bwd_colsum_parts(rows)), dim3(XB_THREADS), 0, s,
+                     (const bf16*)logits, labels, const_cast<float*>(lse_row), stats, grad_out, (bf16*)dlogits,
+                     part, (float*)nullptr, rows, V, ignore_index);
+  DTD_LAUNCH_CHECK();
+}
+
+// Training forward of the mean cross-entropy in one pass over the logits: loss (stats[0]), valid
+// count (stats[1]), lse / loss per row, dlogits for a loss gradient of 1 and the fp32 column
+// partials of dlogits ([parts][V], the bias gradient).  Same shape contract as
+// dtd_xent_bwd_colsum.  The backward scales by the actual loss gradient (dtd_xent_grad_scale).
+DTD_EXPORT int dtd_xent_fwd_train(const void* logits, const int64_t* labels, float* loss_row, float* lse_row,
+                                  float* stats, void* dlogits, float* part, int rows, int V, int ignore_index,
+                                  hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (!dtd_xent_bwd_colsum_supported(V)) return (int)hipErrorInvalidValue;
+  if (((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(dlogits)) & 7) ||
+      (reinterpret_cast<uintptr_t>(part) & 15))
+    return (int)hipErrorInvalidValue;
+  // the valid-label count first (the gradient scale), the loss mean after
+  hipLaunchKernelGGL(xent_reduce_kernel, dim3(1), dim3(1024), 0, s, (const float*)nullptr, labels, rows, ignore_index,
+                     stats);
+  hipLaunchKernelGGL(xent_bwd_colsum_kernel<true>, dim3(dtd_xent_bwd_colsum_parts(rows)), dim3(XB_THREADS), 0, s,
+                     (const bf16*)logits, labels, lse_row, (const float*)stats, (const float*)nullptr,
+                     (bf16*)dlogits, part, loss_row, rows, V, ignore_index);
+  hipLaunchKernelGGL(xent_reduce_kernel, dim3(1), dim3(1024), 0, s, (const float*)loss_row, labels, rows,
+                     ignore_index, stats);
+  DTD_LAUNCH_CHECK();
+}
+
+// x *= g[0] (bf16, in place) unless g[0] == 1: every block reads g and returns at once in the
+// usual case (the loss gradient of a plain loss.backward()).
+__global__ void __launch_bounds__(256) xent_grad_scale_kernel(bf16* __restrict__ x, size_t n,
+                                                              const float* __restrict__ g) {
+  const float sc = g[0];
+  if (sc == 1.f) return;
+  for (size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) * 4; i < n; i += (size_t)gridDim.x * blockDim.x * 4) {
+    if (i + 4 <= n) {
+      bf16x4 v = *reinterpret_cast<const bf16x4*>(x + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (bf16)((float)v[j] * sc);
+      *reinterpret_cast<bf16x4*>(x + i) = v;
+    } else {
+      for (size_t e = i; e < n; ++e) x[e] = (bf16)((float)x[e] * sc);
+    }
+  }
+}
+
+DTD_EXPORT int dtd_xent_grad_scale(void* x, size_t n, const float* g, hipStream_t s) {
+  if (n == 0) return 0;
+  if (reinterpret_cast<uintptr_t>(x) & 7) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(xent_grad_scale_kernel, dim3(1024), dim3(256), 0, s, (bf16*)x, n, g);
   DTD_LAUNCH_CHECK();
 }

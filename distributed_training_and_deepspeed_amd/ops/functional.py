@@ -272,6 +272,38 @@ def xent_fwd(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = IGN
     return stats[0], lse, stats
 
 
+def xent_fwd_train(logits, labels, ignore_index: int = IGNORE_INDEX):
+    """Training forward of the mean cross-entropy in one pass over the logits: returns
+    (loss, lse, stats, dlogits, dbias) with dlogits / dbias (fp32 column sums of dlogits) for a
+    loss gradient of 1 -- ``xent_grad_scale`` applies the actual one in the backward -- or None
+    when the fused kernel does not cover the case (CPU, not bf16, V % 4 != 0, V > 32768)."""
+    V = logits.shape[-1]
+    rows = logits.numel() // V
+    if (not _on_gpu(logits) or logits.dtype != torch.bfloat16 or not logits.is_contiguous() or rows <= 0
+            or logits.data_ptr() % 8 != 0 or not _lib.has("dtd_xent_fwd_train")
+            or not _lib.lib().dtd_xent_bwd_colsum_supported(V)):
+        return None
+    labels = labels.reshape(-1).contiguous().to(torch.int64)
+    loss_row = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    lse = torch.empty_like(loss_row)
+    stats = torch.empty(2, dtype=torch.float32, device=logits.device)
+    d = torch.empty_like(logits)
+    n = _lib.lib().dtd_xent_bwd_colsum_parts(rows)
+    part = torch.empty((n, V), dtype=torch.float32, device=logits.device)
+    _lib.call("dtd_xent_fwd_train", logits.data_ptr(), labels.data_ptr(), loss_row.data_ptr(), lse.data_ptr(),
+              stats.data_ptr(), d.data_ptr(), part.data_ptr(), rows, V, ignore_index, _lib.stream())
+    dbias = torch.empty(V, dtype=torch.float32, device=logits.device)
+    _finalize(part, n, V, dbias, False)
+    return stats[0], lse, stats, d, dbias
+
+
+def xent_grad_scale_(d: torch.Tensor, grad_out: torch.Tensor) -> torch.Tensor:
+    """d *= grad_out in place unless grad_out == 1 (checked on the device: no host sync)."""
+    g = grad_out.reshape(1).to(torch.float32).contiguous()
+    _lib.call("dtd_xent_grad_scale", d.data_ptr(), d.numel(), g.data_ptr(), _lib.stream())
+    return d
+
+
 def xent_bwd(logits, labels, lse, stats, grad_out, ignore_index: int = IGNORE_INDEX, dbias=None):
     """dlogits of the mean cross-entropy.  ``dbias`` = (dst, acc): also the column sums of dlogits
     (the bias gradient of the Linear that produced the logits) -- on the kernel path from the same

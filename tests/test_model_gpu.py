@@ -119,3 +119,35 @@ def test_staged_adam_overlapped_with_forward_is_bit_identical():
     l1, p1 = run(True)
     assert torch.equal(l0, l1), (l0, l1)
     assert torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("gscale", [1.0, 0.5])
+def test_fused_training_cross_entropy_matches_two_pass(gscale):
+    """The MLM head's training forward computes loss, dlogits and the decoder-bias gradient in
+    one pass over the logits (Fx.xent_fwd_train; the backward rescales for a loss gradient other
+    than 1).  Loss and every parameter gradient match the two-pass path (DTD_FUSED_XENT=0)."""
+    from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
+    from distributed_training_and_deepspeed_amd.models import build_model, layers as L
+
+    prev = L._FUSED_XENT[0]
+
+    def run(fused):
+        L._FUSED_XENT[0] = fused
+        try:
+            model = build_model("base", dtype=torch.bfloat16, device="cuda:0", seed=0)
+            ds = SyntheticLMDataset(model.cfg, 2, seq_len=128, seed=0)
+            out = model(ds.input_ids.cuda(), labels=ds.labels.cuda())
+            out.loss.backward(torch.tensor(gscale, device="cuda"))
+            torch.cuda.synchronize()
+            return out.loss.detach().float(), {n: p.grad.float().clone() for n, p in model.named_parameters()
+                                               if p.grad is not None}
+        finally:
+            L._FUSED_XENT[0] = prev
+
+    l0, g0 = run(False)
+    l1, g1 = run(True)
+    assert torch.allclose(l0, l1, rtol=1e-5, atol=1e-5), (l0, l1)
+    assert g0.keys() == g1.keys() and len(g0) > 0
+    for n in g0:
+        err = (g0[n] - g1[n]).norm() / (g0[n].norm() + 1e-12)
+        assert err < 2e-2, (n, err.item())
