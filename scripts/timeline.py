@@ -42,11 +42,18 @@ def union(iv):
     return tot
 
 
+def per_sum(win, cls):
+    return sum(e - s for s, e, n in win if classify(n) == cls)
+
+
 def main(path, nsteps=3):
     rows = list(csv.DictReader(open(path)))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows]
     ks.sort()
-    adam_ends = [e for s, e, n in ks if "adam_kernel" in n]
+    adam = [(s, e) for s, e, n in ks if "adam_kernel" in n]
+    # one step boundary per optimizer step: the last Adam kernel of a burst (the staged optimizer,
+    # FusedAdam.overlap_with_forward, launches one per model stage)
+    adam_ends = [e for i, (s, e) in enumerate(adam) if i + 1 == len(adam) or adam[i + 1][0] - e > 5_000_000]
     if len(adam_ends) < nsteps + 1:
         print("not enough steps")
         return
@@ -64,6 +71,9 @@ def main(path, nsteps=3):
     print(f"per step: wall {ms(span)} ms, busy(all) {ms(busy)} ms, busy(without mask kernels) {ms(nomask)} ms, "
           f"idle {ms(span - busy)} ms")
     print(f"mask kernels {ms(mask_t)} ms/step; exposed (busy - busy_without_mask) {ms(busy - nomask)} ms/step")
+    noadam = union([(s, e) for s, e, n in win if classify(n) != "adam"])
+    print(f"adam kernels {ms(per_sum(win, 'adam'))} ms/step; exposed (busy - busy_without_adam) "
+          f"{ms(busy - noadam)} ms/step")
     for k, v in sorted(per.items(), key=lambda x: -x[1]):
         print(f"  {k:12s} {ms(v):8.3f} ms/step")
 
