@@ -110,12 +110,27 @@ def _write_grad(dst, val: torch.Tensor, acc: bool) -> None:
         dst.copy_(val)
 
 
-def _finalize(part: torch.Tensor, n: int, cols: int, dst, acc: bool, scale: float = 1.0):
+def _finalize_stream(part: torch.Tensor, defer: bool = True) -> int:
+    """Stream for a column-sum finalize of gradient partials.  Inside a DDP backward window
+    (``grad.defer_finalize``) the ~10 us finalize launches go to the async-gradient side stream,
+    off the dgrad chain: the side stream waits for the partials' producer, the partial buffer is
+    recorded on it, and the reducer joins it before any collective or the optimizer reads a
+    gradient (``join_async_wgrad``)."""
+    from .grad import finalize_side_stream
+    side = finalize_side_stream(part.device) if defer and part.is_cuda else None
+    if side is None:
+        return _lib.stream()
+    side.wait_stream(torch.cuda.current_stream(part.device))
+    part.record_stream(side)
+    return side.cuda_stream
+
+
+def _finalize(part: torch.Tensor, n: int, cols: int, dst, acc: bool, scale: float = 1.0, defer: bool = True):
     if dst is None:
         return
     dst, acc = _unpack(dst, acc)
     _lib.call("dtd_colsum_finalize", part.data_ptr(), n, cols, dst.data_ptr(), _lib.dt(dst), int(acc),
-              float(scale), _lib.stream())
+              float(scale), _finalize_stream(part, defer))
 
 
 def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: int,
@@ -169,7 +184,7 @@ def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: i
             else:
                 t, a = _unpack(d, acc)
                 args += [t.data_ptr(), _lib.dt(t), int(a)]
-        _lib.call("dtd_colsum_finalize_multi", len(dsts), part.data_ptr(), n, h, *args, _lib.stream())
+        _lib.call("dtd_colsum_finalize_multi", len(dsts), part.data_ptr(), n, h, *args, _finalize_stream(part))
     return dz, dy
 
 
@@ -293,7 +308,7 @@ def xent_fwd_train(logits, labels, ignore_index: int = IGNORE_INDEX):
     _lib.call("dtd_xent_fwd_train", logits.data_ptr(), labels.data_ptr(), loss_row.data_ptr(), lse.data_ptr(),
               stats.data_ptr(), d.data_ptr(), part.data_ptr(), rows, V, ignore_index, _lib.stream())
     dbias = torch.empty(V, dtype=torch.float32, device=logits.device)
-    _finalize(part, n, V, dbias, False)
+    _finalize(part, n, V, dbias, False, defer=False)   # a forward result, read by the backward
     return stats[0], lse, stats, d, dbias
 
 

@@ -125,6 +125,7 @@ class _AsyncWgrad:
 
     def __init__(self):
         self.enabled = False
+        self.defer_finalize = False
         self.streams: dict = {}
         self.pending = False
 
@@ -144,6 +145,19 @@ def set_async_wgrad(enabled: bool) -> None:
 
 def async_wgrad_enabled() -> bool:
     return _ASYNC.enabled
+
+
+def set_defer_finalize(enabled: bool) -> None:
+    """While on (a DDP backward window: DDP.forward -> DDP.finish), gradient column-sum
+    finalizes run on the async-gradient side stream (ops/functional.py::_finalize_stream)."""
+    _ASYNC.defer_finalize = bool(enabled)
+
+
+def finalize_side_stream(device):
+    if not _ASYNC.defer_finalize:
+        return None
+    _ASYNC.pending = True
+    return _ASYNC.stream(torch.device(device))
 
 
 def join_async_wgrad(device=None) -> None:

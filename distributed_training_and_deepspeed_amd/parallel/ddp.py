@@ -31,13 +31,14 @@ reducer:
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
 from torch import nn
 
 from ..comm import logger as comm_log
-from ..ops.grad import join_async_wgrad, set_async_wgrad
+from ..ops.grad import join_async_wgrad, set_async_wgrad, set_defer_finalize
 from ..ops.grad import _ASYNC as _ASYNC_WGRAD
 from ..runtime import ReadyTracker, assign_buckets
 from .flat import FlatLayout, GradBuffer
@@ -107,6 +108,8 @@ class DistributedDataParallel(nn.Module):
         # bucket collectives are issued from that stream after it joins the compute stream, so
         # neither stream blocks the other; finish() joins it before the optimizer reads grads
         self.async_wgrad = bool(async_wgrad) and self.device.type == "cuda"
+        # gradient column-sum finalizes (bias / LN parameters) on the side stream during backward
+        self._defer_finalize = self.device.type == "cuda" and os.environ.get("DTD_DEFER_FINALIZE", "1") == "1"
         if self.async_wgrad:
             set_async_wgrad(True)
         if broadcast_parameters and self.world > 1:
@@ -145,6 +148,8 @@ class DistributedDataParallel(nn.Module):
         if not self._window_open:   # a new backward window: fresh readiness / launch state
             self.tracker.reset()
             self._window_open = True
+        if self._defer_finalize:
+            set_defer_finalize(True)   # bias / LN-parameter finalizes off the dgrad chain until finish()
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager
@@ -174,6 +179,7 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, b: _Bucket) -> None:
         if self.world == 1:
             return
+        join_async_wgrad(self.device)   # side-stream gradient writers (finalizes, async wgrad)
         view = self.grads.buf[b.start:b.end]
         if self._xgmi is not None and self._xgmi.supports(view):
             join_async_wgrad(self.device)
@@ -204,8 +210,8 @@ class DistributedDataParallel(nn.Module):
     def finish(self) -> None:
         """Launch any bucket not yet launched (unused parameters get zero gradients) and make
         the current stream wait for every all-reduce."""
-        if self.async_wgrad:
-            join_async_wgrad(self.device)
+        join_async_wgrad(self.device)   # async wgrad GEMMs / deferred finalizes
+        set_defer_finalize(False)
         self.grads.zero_untouched_()
         for k in self.tracker.drain():
             self._launch(self.buckets[k])
