@@ -37,7 +37,8 @@ def main():
     tunable.tuning_enable(True)
     tunable.record_untuned_enable(False)
     tunable.set_max_tuning_duration(int(os.environ.get("TUNE_MS", "300")))
-    shapes = ((2304, 768), (768, 768), (3072, 768), (768, 3072))
+    shapes = tuple(tuple(int(v) for v in sh.split("x")) for sh in
+                   os.environ.get("SHAPES", "2304x768,768x768,3072x768,768x3072").split(","))
     data = {}
     for (o, i) in shapes:
         dy = torch.randn(T, o, device="cuda", dtype=bf)
