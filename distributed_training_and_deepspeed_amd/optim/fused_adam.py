@@ -46,6 +46,36 @@ def adam_reference_(p, m, v, g, lr, b1, b2, eps, wd, step, mode, grad_scale=1.0)
         p.addcdiv_(m, v.sqrt().div_(bc2s).add_(eps), value=-lr / bc1)
 
 
+def stage_chunks(spans, nstages: int, n: int) -> list:
+    """Element ranges of a flat buffer [0, n) per optimizer stage.  ``spans``: (start, end, stage)
+    of each parameter.  Returns nstages + 1 lists of merged [a, b) ranges: index 0 holds the
+    elements no stage owns (padding, parameters registered elsewhere), index k + 1 stage k's.  An
+    element shared by several stages (tied parameters) belongs to the first span that covers it;
+    together the lists cover [0, n) exactly once."""
+    chunks = {k: [] for k in range(-1, nstages)}
+    pos = 0
+    for a, b, k in sorted(spans):
+        a = max(a, pos)
+        if a >= b:
+            continue
+        if a > pos:
+            chunks[-1].append((pos, a))
+        chunks[k].append((a, b))
+        pos = b
+    if pos < n:
+        chunks[-1].append((pos, n))
+    out = []
+    for k in range(-1, nstages):
+        merged = []
+        for a, b in sorted(chunks[k]):
+            if merged and merged[-1][1] == a:
+                merged[-1] = (merged[-1][0], b)
+            else:
+                merged.append((a, b))
+        out.append(merged)
+    return out
+
+
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  adam_w_mode: bool = True, bias_correction: bool = True, hf_eps: bool = False,
@@ -190,7 +220,8 @@ class FusedAdam(torch.optim.Optimizer):
         stages' MFMA-bound GEMMs instead of before them.  Elements no stage owns (padding, params
         registered elsewhere) are updated first and waited for by the first stage; a post-hook on
         ``root`` (the whole model; default: the last stage) waits for every chunk before anything
-        after the forward runs (the next backward overwrites the gradients the kernel reads).  Per element the math is the single launch's: results are bit-identical."""
+        after the forward runs (the next backward overwrites the gradients the kernel reads).  Per
+        element the math is the single launch's: results are bit-identical."""
         if not self.master.is_cuda or self._chunks is not None:
             return
         base = self.param_flat
@@ -204,29 +235,7 @@ class FusedAdam(torch.optim.Optimizer):
                 off = p.storage_offset() - base.storage_offset()
                 if 0 <= off and off + p.numel() <= n:
                     spans.append((off, off + p.numel(), k))
-        spans.sort()
-        chunks = {k: [] for k in range(-1, len(stages))}   # -1: elements no stage owns
-        pos = 0
-        for a, b, k in spans:
-            a = max(a, pos)
-            if a >= b:
-                continue   # shared by an earlier stage (tied parameters)
-            if a > pos:
-                chunks[-1].append((pos, a))
-            chunks[k].append((a, b))
-            pos = b
-        if pos < n:
-            chunks[-1].append((pos, n))
-        # merge adjacent ranges of one stage
-        for k, rs in chunks.items():
-            merged = []
-            for a, b in sorted(rs):
-                if merged and merged[-1][1] == a:
-                    merged[-1] = (merged[-1][0], b)
-                else:
-                    merged.append((a, b))
-            chunks[k] = merged
-        self._chunks = [chunks[k] for k in range(-1, len(stages))]
+        self._chunks = stage_chunks(spans, len(stages), n)
         self._side = torch.cuda.Stream(self.master.device)
         self._events = [None] * len(self._chunks)
         self._hooks = []
