@@ -109,7 +109,10 @@ class DistributedDataParallel(nn.Module):
         # neither stream blocks the other; finish() joins it before the optimizer reads grads
         self.async_wgrad = bool(async_wgrad) and self.device.type == "cuda"
         # gradient column-sum finalizes (bias / LN parameters) on the side stream during backward
-        self._defer_finalize = self.device.type == "cuda" and os.environ.get("DTD_DEFER_FINALIZE", "1") == "1"
+        # (world 1 only: at N > 1 every bucket launch would have to join the side stream on the
+        # compute stream, where starved finalizes could stall the dgrad chain)
+        self._defer_finalize = (self.device.type == "cuda" and os.environ.get("DTD_DEFER_FINALIZE", "1") == "1"
+                                and self.world == 1)
         if self.async_wgrad:
             set_async_wgrad(True)
         if broadcast_parameters and self.world > 1:
@@ -179,7 +182,6 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, b: _Bucket) -> None:
         if self.world == 1:
             return
-        join_async_wgrad(self.device)   # side-stream gradient writers (finalizes, async wgrad)
         view = self.grads.buf[b.start:b.end]
         if self._xgmi is not None and self._xgmi.supports(view):
             join_async_wgrad(self.device)
