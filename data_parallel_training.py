@@ -91,8 +91,9 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
         if progress is not None:
             progress.update(len(warm))
 
-    if graphed is None and cuda and hasattr(model, "zero3_units"):
-        # eager steps: the Adam update of later stages overlaps the next forward (bit-identical)
+    if opts.opt_overlap and graphed is None and cuda and hasattr(model, "zero3_units"):
+        # eager steps: the Adam update of later stages overlaps the next forward (bit-identical);
+        # opt-in: see the parameter-access contract of FusedAdam.overlap_with_forward
         optimizer.overlap_with_forward(model.zero3_units(), root=model)
     timer = StepTimer(batch_size * opts.seq_len, world_size)
     start = time.time()
@@ -142,6 +143,8 @@ if __name__ == "__main__":
     parser.add_argument("--markers", action="store_true", help="roctx ranges per phase (rocprofv3 --marker-trace)")
     parser.add_argument("--save-dir", default="", help="write <dir>/ddp_checkpoint.pt at the end")
     parser.add_argument("--resume", default="", help="checkpoint file to resume from")
+    parser.add_argument("--opt-overlap", action="store_true",
+                        help="stage the Adam update under the next forward (FusedAdam.overlap_with_forward)")
     parser.add_argument("--graph", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
                         help="capture the whole training step in a hipGraph and replay it (auto: on for one GPU "
                              "at <= 32 sequences per step, where the step is host-launch bound)")

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -81,15 +82,23 @@ def init(rank: int | None = None, world_size: int | None = None, backend: str | 
     return rank, world_size
 
 
-def destroy() -> None:
+def destroy(barrier: bool | None = None) -> None:
     """Orderly teardown: every rank reaches the barrier before any rank closes its transport.
     (Without it a fast rank's exit can close gloo pairs under a peer that is still finishing
-    its last collective; that peer's transport thread then aborts the process.)"""
-    if dist.is_initialized():
-        try:
+    its last collective; that peer's transport thread then aborts the process.)
+
+    ``barrier=None`` skips the barrier when called while an exception is propagating (a
+    ``finally`` block on an error path): a dead or stuck peer would otherwise hold every
+    surviving rank for the whole process-group timeout."""
+    if not dist.is_initialized():
+        return
+    if barrier is None:
+        barrier = sys.exc_info()[0] is None
+    try:
+        if barrier:
             dist.barrier()
-        finally:
-            dist.destroy_process_group()
+    finally:
+        dist.destroy_process_group()
 
 
 def rank() -> int:

@@ -265,6 +265,13 @@ DTD_EXPORT int dtd_xgmi_error(void* ctx, hipStream_t s) {
   return (int)v;
 }
 
+// Non-blocking form: queue a copy of the error flag into `host_dst` (pinned host memory) on `s`.
+// The caller reads the value one step later, so no host synchronisation is needed per step.
+DTD_EXPORT int dtd_xgmi_error_poll(void* ctx, uint32_t* host_dst, hipStream_t s) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  return (int)hipMemcpyAsync(host_dst, c->err, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+}
+
 // y = scale * sum over ranks of x (per virtual rank in local mode: ins/outs arrays of `local` pointers).
 // dtype: 0 fp32, 1 bf16.  mode: 0 one-shot, 1 two-shot.  numel % 8 == 0 (two-shot: % (8 world)).
 DTD_EXPORT int dtd_xgmi_allreduce(void* ctx, const void* const* ins, void* const* outs, long long numel, int dtype,

@@ -197,6 +197,44 @@ def all_gather_into_tensor(output, input, group=None, async_op=False):
                             output, _nbytes(output), group, async_op)
 
 
+class _MultiWork:
+    """Work handle over several collectives (the gloo fallback of the coalesced calls)."""
+
+    def __init__(self, works):
+        self.works = [w for w in works if w is not None]
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return True
+
+    def is_completed(self):
+        return all(w.is_completed() for w in self.works)
+
+
+def all_gather_coalesced(outputs, inputs, group=None, async_op=False):
+    """Several ``all_gather_into_tensor`` calls as ONE RCCL group launch (ncclGroupStart/End via
+    torch's coalescing manager) on the nccl backend; one call each elsewhere.  Logged as one
+    all_gather_into_tensor of the summed size (DeepSpeed's ``allgather_bucket_size`` unit)."""
+    outputs, inputs = list(outputs), list(inputs)
+    nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
+
+    def fn(a):
+        if nccl and len(outputs) > 1:
+            with dist._coalescing_manager(group=group, device=outputs[0].device, async_ops=True) as cm:
+                for o, i in zip(outputs, inputs):
+                    dist.all_gather_into_tensor(o, i, group=group)
+            if a:
+                return cm
+            cm.wait()
+            return None
+        works = [dist.all_gather_into_tensor(o, i, group=group, async_op=a) for o, i in zip(outputs, inputs)]
+        return _MultiWork(works) if a else None
+
+    return comms_logger.run("all_gather_into_tensor", fn, outputs[0] if outputs else None,
+                            sum(_nbytes(o) for o in outputs), group, async_op)
+
+
 def all_to_all_single(output, input, group=None, async_op=False):
     return comms_logger.run("all_to_all_single",
                             lambda a: dist.all_to_all_single(output, input, group=group, async_op=a),

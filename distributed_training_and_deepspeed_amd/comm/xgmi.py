@@ -42,6 +42,7 @@ _SIGS = {
     "dtd_xgmi_open": (ctypes.c_int, [P, P]),
     "dtd_xgmi_destroy": (ctypes.c_int, [P]),
     "dtd_xgmi_error": (ctypes.c_int, [P, P]),
+    "dtd_xgmi_error_poll": (ctypes.c_int, [P, P, P]),
     "dtd_xgmi_allreduce": (ctypes.c_int, [P, P, P, ctypes.c_longlong, ctypes.c_int, ctypes.c_int, ctypes.c_uint,
                                           ctypes.c_float, ctypes.c_int, P]),
 }
@@ -134,6 +135,16 @@ class XgmiAllReduce:
     def error(self) -> bool:
         """True if a barrier timed out (a peer never arrived) since creation."""
         return bool(self.lib.dtd_xgmi_error(self.ctx, _lib.stream()))
+
+    def error_poll(self) -> bool:
+        """Non-blocking check: True if a barrier timeout was seen by an EARLIER poll.  Each call
+        reads the pinned host word that the previous call's async copy filled, then queues a new
+        copy on the current stream -- the exposure window is the one step between polls."""
+        if getattr(self, "_herr", None) is None:
+            self._herr = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        seen = bool(int(self._herr[0]))
+        self.lib.dtd_xgmi_error_poll(self.ctx, self._herr.data_ptr(), _lib.stream())
+        return seen
 
     def close(self) -> None:
         if self.ctx:

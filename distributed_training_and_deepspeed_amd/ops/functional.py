@@ -364,6 +364,37 @@ def xent_bwd(logits, labels, lse, stats, grad_out, ignore_index: int = IGNORE_IN
     return d
 
 
+class _CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        loss, lse, stats = xent_fwd(logits, labels, ignore_index)
+        ctx.save_for_backward(logits, labels, lse, stats)
+        ctx.ignore_index = ignore_index
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        logits, labels, lse, stats = ctx.saved_tensors
+        return xent_bwd(logits, labels, lse, stats, gloss, ctx.ignore_index), None, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = IGNORE_INDEX) -> torch.Tensor:
+    """Mean softmax cross-entropy over rows of ``logits`` [..., V] straight from the logits' own
+    dtype (bf16: no fp32 up-cast copy of the logits; the kernel accumulates in fp32) -- the
+    drop-in for ``nn.CrossEntropyLoss()(logits.view(-1, V).float(), labels.view(-1))`` of
+    /root/reference/model_parallel_training.py:51,73."""
+    return _CrossEntropyFn.apply(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), ignore_index)
+
+
+class CrossEntropyLoss(torch.nn.Module):
+    def __init__(self, ignore_index: int = IGNORE_INDEX):
+        super().__init__()
+        self.ignore_index = ignore_index
+
+    def forward(self, logits, labels):
+        return cross_entropy(logits, labels, self.ignore_index)
+
+
 # --------------------------------------------------------------------------------------
 # embeddings
 # --------------------------------------------------------------------------------------

@@ -221,7 +221,14 @@ class FusedAdam(torch.optim.Optimizer):
         registered elsewhere) are updated first and waited for by the first stage; a post-hook on
         ``root`` (the whole model; default: the last stage) waits for every chunk before anything
         after the forward runs (the next backward overwrites the gradients the kernel reads).  Per
-        element the math is the single launch's: results are bit-identical."""
+        element the math is the single launch's: results are bit-identical.
+
+        Contract: between step() and the end of the next forward of ``root``, a parameter may be
+        read only inside the forward of its own stage (after that stage's pre-hook).  Code that
+        reads weights elsewhere -- a submodule method called directly, EMA / logging of weights,
+        evaluation through submodules -- must call ``synchronize()`` first (state_dict,
+        load_state_dict and checkpoint saving do).  The scripts enable this only where the
+        training loop honours that (bench.py; data_parallel_training.py ``--opt-overlap``)."""
         if not self.master.is_cuda or self._chunks is not None:
             return
         base = self.param_flat
@@ -276,6 +283,11 @@ class FusedAdam(torch.optim.Optimizer):
                 ev = torch.cuda.Event()
                 ev.record(side)
                 self._events[i] = ev
+
+    def parameters_ready(self) -> None:
+        """Public fence for code that reads parameters outside a stage forward (see the
+        contract of overlap_with_forward): the current stream waits for every staged update."""
+        self.synchronize()
 
     def zero_grad(self, set_to_none: bool = True):
         if self.gbuf is not None:

@@ -94,8 +94,10 @@ class DistributedDataParallel(nn.Module):
         self.backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
         self._xgmi = None
         # a timed-out xGMI barrier (a peer never arrived) leaves the bucket holding a sum over
-        # stale peer data; the kernel only raises a device flag, so finish() reads it every
-        # ``xgmi_check_every`` synced steps (one host sync) and raises
+        # stale peer data; the kernel only raises a device flag.  finish() polls it every synced
+        # step without a host sync (an async copy into pinned memory, read one step later), so
+        # at most one optimizer step applies corrupt gradients before the run raises; every
+        # ``xgmi_check_every`` steps it also does a blocking read
         self._xgmi_check_every = max(1, int(xgmi_check_every))
         self._xgmi_steps = 0
         if small_bucket_allreduce == "xgmi" and self.world > 1 and self.backend == "nccl":
@@ -108,10 +110,12 @@ class DistributedDataParallel(nn.Module):
         # bucket collectives are issued from that stream after it joins the compute stream, so
         # neither stream blocks the other; finish() joins it before the optimizer reads grads
         self.async_wgrad = bool(async_wgrad) and self.device.type == "cuda"
-        # gradient column-sum finalizes (bias / LN parameters) on the side stream during backward
-        # (world 1 only: at N > 1 every bucket launch would have to join the side stream on the
-        # compute stream, where starved finalizes could stall the dgrad chain)
-        self._defer_finalize = (self.device.type == "cuda" and os.environ.get("DTD_DEFER_FINALIZE", "1") == "1"
+        # gradient column-sum finalizes (bias / LN parameters) on the side stream during backward:
+        # opt-in (DTD_DEFER_FINALIZE=1) and world 1 only.  It measured +0.15 % at b256
+        # (profiles/r2_ab_defer_finalize.jsonl); off by default so the 1-GPU bench runs the same
+        # stream schedule as the N > 1 path, where every bucket launch would have to join the
+        # side stream on the compute stream
+        self._defer_finalize = (self.device.type == "cuda" and os.environ.get("DTD_DEFER_FINALIZE", "0") == "1"
                                 and self.world == 1)
         if self.async_wgrad:
             set_async_wgrad(True)
@@ -151,8 +155,10 @@ class DistributedDataParallel(nn.Module):
         if not self._window_open:   # a new backward window: fresh readiness / launch state
             self.tracker.reset()
             self._window_open = True
-        if self._defer_finalize:
-            set_defer_finalize(True)   # bias / LN-parameter finalizes off the dgrad chain until finish()
+        if self._defer_finalize and torch.is_grad_enabled():
+            # bias / LN-parameter finalizes off the dgrad chain until the end of this backward
+            # (_finish_backward joins them, synced or not)
+            set_defer_finalize(True)
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager
@@ -206,6 +212,10 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._window_open = False
         if not self._sync_enabled:
+            # a no_sync micro-step: its side-stream finalizes wrote main_grad; join them before
+            # anything else (logging, the next micro-step's autograd-path adds) touches it
+            join_async_wgrad(self.device)
+            set_defer_finalize(False)
             return
         self.finish()
 
@@ -228,7 +238,7 @@ class DistributedDataParallel(nn.Module):
         self._need_reset = True
         if self._xgmi is not None:
             self._xgmi_steps += 1
-            if self._xgmi_steps % self._xgmi_check_every == 0:
+            if self._xgmi.error_poll() or self._xgmi_steps % self._xgmi_check_every == 0:
                 self.check_xgmi()
 
     def check_xgmi(self) -> None:

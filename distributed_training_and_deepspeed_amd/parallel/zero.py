@@ -3,7 +3,7 @@
 Reference: ``deepspeed.initialize(model, model_parameters, config)`` -> (engine, optimizer, _, _),
 ``engine(input_ids, labels=...)``, ``engine.backward(loss)``, ``engine.step()``,
 ``engine.zero_optimization_stage()`` and ``optimizer.param_groups[0]`` printing the *local*
-partition size (zero_dp_training.py:26-57,81-94).
+partition size (/root/reference/zero_dp_training.py:26-57,81-94).
 
 MI355X-first design (flat buffers, RCCL collectives on contiguous slices, no flatten copies):
 
@@ -16,15 +16,23 @@ MI355X-first design (flat buffers, RCCL collectives on contiguous slices, no fla
 * stage 0: segments = ``allreduce_bucket_size`` buckets, gradients all-reduced (replicated
   optimizer state, DeepSpeed's "stage 0").
 * stage 1: optimizer states partitioned; full gradient buffer, reduce-scatter after backward.
-* stage 2: + gradients partitioned: a bucket's gradient landing buffer is allocated from the
-  caching allocator on its first write, reduce-scattered on the comm stream as soon as the
-  bucket is complete (overlapping the rest of backward) and released -- only the local
-  gradient shard persists.
+* stage 2: + gradients partitioned: a bucket's gradient landing region is taken from a
+  persistent ring arena (``_Arena``) on its first write, reduce-scattered on the comm stream as
+  soon as the bucket is complete (overlapping the rest of backward) and handed back with an
+  event -- only the local gradient shard persists, and no buffer is allocated per step (the
+  whole step is hipGraph-capturable).
 * stage 3: + parameters partitioned: every model unit (embeddings, each transformer layer,
-  head) keeps only its parameter shard; the unit is all-gathered on the comm stream before
-  its forward/backward (with one-unit-ahead prefetch) and released after, and its gradients
-  are reduce-scattered as soon as its backward finishes.  Parameters shared between units
-  (tied word embeddings) stay replicated with stage-2 treatment.
+  head) keeps only its parameter shard; the unit is all-gathered into a gather arena on a
+  SEPARATE communicator (``gather_group``: its RCCL stream runs beside the reduce-scatters
+  instead of queueing behind them) before its forward/backward, with prefetch up to
+  ``stage3_prefetch_bucket_size`` elements ahead, released after use, and its gradients are
+  reduce-scattered as soon as its backward finishes.  Parameters shared between units (tied
+  word embeddings) stay replicated with stage-2 treatment.
+* After ``step()`` (stages >= 1) the updated shards are all-gathered back into the replicated
+  buckets in FORWARD order, ``allgather_bucket_size`` elements per coalesced RCCL launch, each
+  group recording an event; the next forward's per-unit pre-hooks wait only for the events of
+  the buckets holding that unit's parameters, so the refresh of later layers overlaps the
+  forward of earlier ones (DeepSpeed waits for the whole all-gather inside ``step()``).
 * Collectives go through ``comm.logger`` (the DeepSpeed comms-logger equivalent).
 """
 from __future__ import annotations
@@ -50,7 +58,8 @@ DEFAULTS = {
     "optimizer": {"type": "Adam", "params": {"lr": 1e-3}},
     "comms_logger": {"enabled": False},
     "zero_optimization": {"stage": 0, "reduce_bucket_size": 5e8, "allgather_bucket_size": 5e8,
-                          "overlap_comm": None, "stage3_prefetch_bucket_size": 5e7},
+                          "overlap_comm": None, "stage3_prefetch_bucket_size": 5e7,
+                          "overlap_param_refresh": True},
 }
 
 
@@ -73,7 +82,9 @@ class ZeroConfig:
             raise ValueError(f"ZeRO stage must be 0-3, got {self.stage}")
         self.reduce_bucket = int(float(z.get("reduce_bucket_size", 5e8)))
         self.allreduce_bucket = int(float(cfg.get("allreduce_bucket_size", z.get("allreduce_bucket_size", 5e8))))
-        self.allgather_bucket = int(float(z.get("allgather_bucket_size", 5e8)))
+        self.allgather_bucket = max(1, int(float(z.get("allgather_bucket_size", 5e8))))
+        self.prefetch_bucket = max(0, int(float(z.get("stage3_prefetch_bucket_size", 5e7))))
+        self.overlap_refresh = bool(z.get("overlap_param_refresh", True))
         oc = z.get("overlap_comm")
         self.overlap = (self.stage >= 2) if oc is None else bool(oc)
         bf = cfg.get("bf16", {})
@@ -82,7 +93,7 @@ class ZeroConfig:
 
 class _Segment:
     __slots__ = ("index", "params", "shapes", "offsets", "numel", "chunk", "shard_off", "full", "gbuf", "ready",
-                 "launched", "unit", "gather_event", "module", "pending_release")
+                 "launched", "unit", "gather_event", "module", "pending_release", "first_use")
 
     def __init__(self, index, params, world):
         self.index = index
@@ -96,14 +107,15 @@ class _Segment:
         self.numel = max(q, -(-off // q) * q)
         self.chunk = self.numel // world
         self.shard_off = 0
-        self.full = None      # full param buffer (persistent: view into flat; unit: gathered tensor)
-        self.gbuf = None      # full gradient landing buffer
+        self.full = None      # full param buffer (persistent: view into flat; unit: gathered region)
+        self.gbuf = None      # full gradient landing region
         self.ready = 0
         self.launched = False
         self.unit = False
         self.gather_event = None
         self.module = None
         self.pending_release = False
+        self.first_use = 0    # forward position of the first unit that reads this segment
 
     def view(self, flat: torch.Tensor, i: int) -> torch.Tensor:
         shape = self.shapes[i]
@@ -125,6 +137,89 @@ def _split_buckets(params, cap_elems: int):
     return buckets
 
 
+class _Arena:
+    """Ring sub-allocator over ONE persistent buffer (ZeRO-2/3 gradient landing regions and
+    ZeRO-3 gathered-parameter regions).
+
+    ``acquire(n, key)`` returns a region at the ring head (wrapping to 0 when it does not fit),
+    skipping past regions still live; ``release(t, event)`` hands a region back together with
+    the event after which it may be overwritten, and the next acquirer of overlapping bytes makes
+    its stream wait for that event.  Requests larger than half the arena get a dedicated
+    persistent buffer per ``key`` (a BLOOM word-embedding gradient), and a request that finds no
+    free range falls back to the caching allocator.  The sequence of requests is the same every
+    step, so after the first step the addresses are too: nothing is allocated per step and the
+    step can be captured in a hipGraph.  ``new_window()`` drops the previous step's events
+    (callers order the new step behind the old one with a stream wait)."""
+
+    def __init__(self, numel: int, dtype, device):
+        self.numel = max(int(numel), 0)
+        self.dtype, self.device = dtype, device
+        self.buf = torch.empty(self.numel, dtype=dtype, device=device) if self.numel else None
+        self.head = 0
+        self.live = {}       # start -> end of regions handed out and not released
+        self.done = []       # (start, end, event or None) released regions
+        self.dedicated = {}  # key -> [tensor, event, live]
+        self.heap_fallbacks = 0
+
+    def _base(self) -> int:
+        return self.buf.data_ptr() if self.buf is not None else 0
+
+    def new_window(self) -> None:
+        self.done = [(a, b, None) for a, b, _ in self.done]
+        for d in self.dedicated.values():
+            d[1] = None
+
+    def acquire(self, n: int, key, waiter=None) -> torch.Tensor:
+        """A region of ``n`` elements; ``waiter(event)`` is called for every release event that
+        guards the returned bytes (the caller makes its stream wait)."""
+        if n > self.numel // 2:
+            d = self.dedicated.get(key)
+            if d is None:
+                d = self.dedicated[key] = [torch.empty(n, dtype=self.dtype, device=self.device), None, False]
+            if d[1] is not None and waiter is not None:
+                waiter(d[1])
+            d[1], d[2] = None, True
+            return d[0]
+        a = self.head if self.head + n <= self.numel else 0
+        for _ in range(len(self.live) + 2):
+            hit = [e for st, e in self.live.items() if st < a + n and a < e]
+            if not hit:
+                break
+            a = max(hit)
+            if a + n > self.numel:
+                a = 0
+        else:
+            hit = True
+        if hit or a + n > self.numel:
+            self.heap_fallbacks += 1
+            return torch.empty(n, dtype=self.dtype, device=self.device)
+        keep = []
+        for st, e, ev in self.done:
+            if st < a + n and a < e:
+                if ev is not None and waiter is not None:
+                    waiter(ev)
+            else:
+                keep.append((st, e, ev))
+        self.done = keep
+        self.live[a] = a + n
+        self.head = a + n
+        return self.buf[a:a + n]
+
+    def release(self, t: torch.Tensor, event=None, stream=None) -> None:
+        for d in self.dedicated.values():
+            if d[0].data_ptr() == t.data_ptr() and d[2]:
+                d[1], d[2] = event, False
+                return
+        if self.buf is not None:
+            es = t.element_size()
+            a = (t.data_ptr() - self._base()) // es
+            if 0 <= a < self.numel and a in self.live:
+                self.done.append((a, self.live.pop(a), event))
+                return
+        if stream is not None and t.is_cuda:   # a caching-allocator fallback region
+            t.record_stream(stream)
+
+
 class ZeroEngine(nn.Module):
     def __init__(self, model: nn.Module, config: dict | None = None, model_parameters=None, process_group=None):
         super().__init__()
@@ -144,12 +239,22 @@ class ZeroEngine(nn.Module):
         self.grad_dtype = p0.dtype
         self.cuda = self.device.type == "cuda"
         self.comm_stream = torch.cuda.Stream(self.device) if self.cuda else None
+        # stage 3 gathers: their own stream AND their own communicator (one RCCL stream per
+        # process group), so a prefetch gather does not queue behind a reduce-scatter
+        self.gather_stream = torch.cuda.Stream(self.device) if (self.cuda and self.stage == 3) else None
+        self.gather_group = process_group
+        if self.stage == 3 and self.world > 1:
+            ranks = dist.get_process_group_ranks(process_group) if process_group is not None \
+                else list(range(self.world))
+            self.gather_group = dist.new_group(ranks=ranks)
         self.shard_world = 1 if self.stage == 0 else self.world
         self.shard_rank = 0 if self.stage == 0 else self.rank
         self.micro_step = 0
         self.global_steps = 0
         self._callback_queued = False
         self._need_reset = True
+        self._refresh_events = {}   # segment index -> event of its last refresh all-gather
+        self._refresh_waits = {}    # id(module) -> segment indices its forward reads
 
         # ---- partition parameters into persistent buckets and (stage 3) units
         units, persistent = [], params
@@ -185,6 +290,7 @@ class ZeroEngine(nn.Module):
         self._broadcast_initial(params)
         self._build_storage()
         self._install_grad_hooks()
+        self._plan_refresh(model)
         if self.stage == 3:
             self._install_unit_hooks()
         self.optimizer = self._build_optimizer()
@@ -209,11 +315,86 @@ class ZeroEngine(nn.Module):
         persistent = [p for p in params if id(p) not in placed]
         return units, persistent
 
+    def _plan_refresh(self, model) -> None:
+        """Forward order of the replicated buckets and the per-unit waits of the overlapped
+        parameter refresh (stages >= 1).  A bucket's forward position is that of the first unit
+        (``model.zero3_units()``, forward order) reading one of its parameters; buckets no unit
+        reads are waited for before the forward starts."""
+        mods = list(model.zero3_units()) if hasattr(model, "zero3_units") else []
+        first = {}
+        for k, m in enumerate(mods):
+            seen = set()
+            for p in m.parameters():
+                hit = self._seg_of.get(id(p))
+                if hit is None or hit[0].unit:
+                    continue
+                s = hit[0]
+                first.setdefault(s.index, k)
+                seen.add(s.index)
+            if seen:
+                self._refresh_waits[id(m)] = sorted(seen)
+        for s in self.buckets:
+            s.first_use = first.get(s.index, -1)
+        # forward order; ties (and buckets no unit reads, first_use -1, first) by reverse bucket
+        # order = registration order
+        fwd = sorted(self.buckets, key=lambda s: (s.first_use, -s.index))
+        cap = self.config.allgather_bucket
+        self._refresh_groups, cur, size = [], [], 0
+        for s in fwd:
+            if cur and size + s.numel > cap:
+                self._refresh_groups.append(cur)
+                cur, size = [], 0
+            cur.append(s)
+            size += s.numel
+        if cur:
+            self._refresh_groups.append(cur)
+        self._overlap_refresh = (self.config.overlap_refresh and self.cuda and self.stage >= 1 and bool(mods))
+        if self._overlap_refresh:
+            for m in mods:
+                if id(m) in self._refresh_waits:
+                    m.register_forward_pre_hook(self._make_refresh_wait(self._refresh_waits[id(m)]))
+
+    def _make_refresh_wait(self, idx):
+        def hook(mod, args):
+            self._wait_refresh(idx)
+        return hook
+
+    def _wait_refresh(self, idx=None) -> None:
+        """Make the compute stream wait for the refresh all-gathers of segments ``idx`` (all when
+        None).  Each event is waited for once."""
+        if not self._refresh_events:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for k in (list(self._refresh_events) if idx is None else idx):
+            ev = self._refresh_events.pop(k, None)
+            if ev is not None:
+                cur.wait_event(ev)
+
     @torch.no_grad()
     def _broadcast_initial(self, params) -> None:
-        if self.world > 1:
-            for p in params:  # C6: every rank starts from rank 0's weights
-                clog.broadcast(p.data, src=0, group=self.group)
+        """C6: every rank starts from rank 0's weights -- one broadcast per <= 256 MiB flat chunk
+        of each dtype (DDP's 250 MiB coalescing), not one per parameter."""
+        if self.world <= 1:
+            return
+        by_dtype = {}
+        for p in params:
+            by_dtype.setdefault(p.dtype, []).append(p)
+        for dt, ps in by_dtype.items():
+            es = torch.empty(0, dtype=dt).element_size()
+            cap = max(1, (256 << 20) // es)
+            chunk, n = [], 0
+            for p in ps + [None]:
+                if p is None or (chunk and n + p.numel() > cap):
+                    flat = torch.cat([q.data.reshape(-1) for q in chunk])
+                    clog.broadcast(flat, src=0, group=self.group)
+                    off = 0
+                    for q in chunk:
+                        q.data.copy_(flat[off:off + q.numel()].view_as(q))
+                        off += q.numel()
+                    chunk, n = [], 0
+                if p is not None:
+                    chunk.append(p)
+                    n += p.numel()
 
     # ================================================================== storage
     @torch.no_grad()
@@ -244,6 +425,13 @@ class ZeroEngine(nn.Module):
                 for i, p in enumerate(s.params):
                     p.main_grad = s.view(s.gbuf, i)
                 off += s.numel
+        # ring arenas: gradient landing regions (stages 2/3) and gathered units (stage 3)
+        reg = [s.numel for s in self.segments if self.stage >= 2 or s.unit]
+        big_unit = max([s.numel for s in self.units], default=0)
+        self.landing = _Arena(max(4 * max(self.config.reduce_bucket, ALIGN), 3 * big_unit) if reg else 0,
+                              self.grad_dtype, dev)
+        self.gather_arena = _Arena(max(self.config.prefetch_bucket + 2 * big_unit, 4 * big_unit) if self.units else 0,
+                                   dt, dev)
         # master shard: chunk `shard_rank` of every segment
         for s in self.buckets:
             lo = self.shard_rank * s.chunk
@@ -258,7 +446,8 @@ class ZeroEngine(nn.Module):
             self.master[s.shard_off:s.shard_off + s.chunk].copy_(full[lo:lo + s.chunk])
             if self.lowp is not None:
                 self.lowp[s.shard_off:s.shard_off + s.chunk].copy_(full[lo:lo + s.chunk])
-            self._set_released(s)
+            for p in s.params:
+                p.data = torch.empty(0, dtype=self.dtype, device=self.device)
         if self.stage == 0:
             # replicated optimizer: the shard IS the whole flat buffer -- alias instead of copying
             self.gshard = self.grad_flat
@@ -327,7 +516,10 @@ class ZeroEngine(nn.Module):
             self._alloc_landing(s)
 
     def _alloc_landing(self, s: _Segment) -> None:
-        s.gbuf = torch.zeros(s.numel, dtype=self.grad_dtype, device=self.device)
+        cur = torch.cuda.current_stream(self.device) if self.cuda else None
+        s.gbuf = self.landing.acquire(s.numel, s.index, waiter=cur.wait_event if cur is not None else None)
+        # padding (alignment gaps, segment tail) must reduce as zeros: the region is recycled
+        s.gbuf.zero_()
         for i, p in enumerate(s.params):
             p.main_grad = s.view(s.gbuf, i)
             p._dtd_touched = False
@@ -348,15 +540,16 @@ class ZeroEngine(nn.Module):
             elif not s.launched:
                 self._reduce_segment(s)
 
-    def _comm_ctx(self):
-        if self.comm_stream is None:
+    def _comm_ctx(self, stream=None):
+        stream = stream if stream is not None else self.comm_stream
+        if stream is None:
             return contextlib.nullcontext()
-        self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
-        return torch.cuda.stream(self.comm_stream)
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        return torch.cuda.stream(stream)
 
     def _reduce_segment(self, s: _Segment) -> None:
         """Reduce one segment's gradients: all-reduce (stage 0) or reduce-scatter into the
-        local gradient shard (stages 1-3); stage 2/3 landing buffers are released after."""
+        local gradient shard (stages 1-3); stage 2/3 landing regions go back to the arena."""
         s.launched = True
         for p in s.params:  # parameters without a gradient this step contribute zeros
             if not p._dtd_touched and s.gbuf is not None:
@@ -388,9 +581,12 @@ class ZeroEngine(nn.Module):
                     dst.copy_(buf)
                 if not first:
                     out.add_(dst)
+            ev = None
+            if self.comm_stream is not None and (self.stage >= 2 or s.unit):
+                ev = torch.cuda.Event()
+                ev.record(self.comm_stream)
         if self.stage >= 2 or s.unit:
-            if self.comm_stream is not None:
-                buf.record_stream(self.comm_stream)
+            self.landing.release(buf, ev, self.comm_stream)
             s.gbuf = None
             for p in s.params:
                 p.main_grad = None
@@ -423,17 +619,17 @@ class ZeroEngine(nn.Module):
     def _gather(self, s: _Segment) -> None:
         if s.full is not None:
             return
-        full = torch.empty(s.numel, dtype=self.dtype, device=self.device)
+        full = self.gather_arena.acquire(s.numel, s.index)
         src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
-        with self._comm_ctx():
+        with self._comm_ctx(self.gather_stream):   # the stream wait orders it behind earlier reads
             if self.world > 1:
-                w = clog.all_gather_into_tensor(full, src, group=self.group, async_op=True)
+                w = clog.all_gather_into_tensor(full, src, group=self.gather_group, async_op=True)
                 w.wait()
             else:
                 full.copy_(src)
-            if self.comm_stream is not None:
+            if self.gather_stream is not None:
                 ev = torch.cuda.Event()
-                ev.record(self.comm_stream)
+                ev.record(self.gather_stream)
                 s.gather_event = ev
         s.full = full
         for i, p in enumerate(s.params):
@@ -448,17 +644,30 @@ class ZeroEngine(nn.Module):
     def _release(self, s: _Segment) -> None:
         if s.full is None:
             return
-        if self.cuda:
-            s.full.record_stream(torch.cuda.current_stream(self.device))
+        if s.gather_event is not None:   # gathered (prefetched) but never used: still order it
+            torch.cuda.current_stream(self.device).wait_event(s.gather_event)
+            s.gather_event = None
+        self.gather_arena.release(s.full, None,
+                                  torch.cuda.current_stream(self.device) if self.cuda else None)
         self._set_released(s)
+
+    def _prefetch(self, order) -> None:
+        """Gather the units of ``order`` (the next ones to run) while the elements gathered
+        ahead stay within ``stage3_prefetch_bucket_size`` -- at least one unit ahead."""
+        ahead = 0
+        for j, u in enumerate(order):
+            if j > 0 and ahead + u.numel > self.config.prefetch_bucket:
+                break
+            if u.full is None:
+                self._gather(u)
+            ahead += u.numel
 
     def _make_pre_fwd(self, k: int):
         def hook(mod, args):
             if self._need_reset:
                 self._reset()
             self._ensure(self.units[k])
-            if k + 1 < len(self.units):
-                self._gather(self.units[k + 1])  # prefetch the next unit
+            self._prefetch(self.units[k + 1:])
         return hook
 
     def _make_post_fwd(self, k: int):
@@ -478,8 +687,7 @@ class ZeroEngine(nn.Module):
             self._ensure(s)
             if s.gbuf is None:
                 self._alloc_landing(s)
-            if k > 0:
-                self._gather(self.units[k - 1])  # prefetch the previous unit for its backward
+            self._prefetch(self.units[:k][::-1])
             return grad
         return hook
 
@@ -502,6 +710,8 @@ class ZeroEngine(nn.Module):
     def _reset(self) -> None:
         accumulate_full = self.stage <= 1 and self.micro_step > 0  # keep accumulating in place
         self.tracker.reset()
+        self.landing.new_window()
+        self.gather_arena.new_window()
         for s in self.segments:
             s.launched = False
             for p in s.params:
@@ -514,7 +724,15 @@ class ZeroEngine(nn.Module):
     def forward(self, *args, **kwargs):
         if self._need_reset:
             self._reset()
-        return self.module(*args, **kwargs)
+        if self._refresh_events and self.cuda and torch.cuda.is_current_stream_capturing():
+            self._refresh_events.clear()   # recorded before the capture (which starts synchronised)
+        if self._refresh_events:
+            # buckets no unit reads (and every bucket when the model has no units) first; the
+            # units' pre-hooks wait for their own buckets while the later refreshes land
+            self._wait_refresh([s.index for s in self.buckets if s.first_use < 0])
+        out = self.module(*args, **kwargs)
+        self._wait_refresh()   # the backward reads every weight
+        return out
 
     def backward(self, loss: torch.Tensor) -> None:
         if self.config.gas > 1:
@@ -541,24 +759,38 @@ class ZeroEngine(nn.Module):
             rt.rng.advance()
 
     @torch.no_grad()
-    def _refresh_params(self) -> None:
-        """Stage 0: the kernel wrote the replicated params; stages 1-2: all-gather each
-        bucket from the updated shards; stage 3 units stay sharded until their next use."""
+    def _refresh_params(self, wait: bool | None = None) -> None:
+        """Stage 0: the kernel wrote the replicated params; stages 1-2 (and stage 3's replicated
+        buckets): all-gather the updated shards into the buckets in forward order, one coalesced
+        RCCL launch per ``allgather_bucket_size`` group on the comm stream.  With the overlapped
+        refresh each group records an event and the next forward's unit pre-hooks wait for their
+        own buckets only; otherwise the compute stream waits for everything here.  Stage 3 units
+        stay sharded until their next use."""
         if self.stage == 0:
             for s in self.buckets:
                 src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
                 if src.data_ptr() != s.full.data_ptr():   # aliased (the usual case): nothing to copy
                     s.full.copy_(src)
             return
-        for s in self.buckets:
-            src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
-            if self.world > 1:
-                with self._comm_ctx():
-                    w = clog.all_gather_into_tensor(s.full, src, group=self.group, async_op=True)
+        wait = (not self._overlap_refresh) if wait is None else wait
+        if self.cuda and torch.cuda.is_current_stream_capturing():
+            wait = True   # a captured step must join its side-stream work before it ends
+        for grp in self._refresh_groups:
+            with self._comm_ctx():
+                outs = [s.full for s in grp]
+                ins = [self.lowp_view[s.shard_off:s.shard_off + s.chunk] for s in grp]
+                if self.world > 1:
+                    w = clog.all_gather_coalesced(outs, ins, group=self.group, async_op=True)
                     w.wait()
-            else:
-                s.full.copy_(src)
-        if self.comm_stream is not None:
+                else:
+                    for o, i in zip(outs, ins):
+                        o.copy_(i)
+                if self.comm_stream is not None and not wait:
+                    ev = torch.cuda.Event()
+                    ev.record(self.comm_stream)
+                    for s in grp:
+                        self._refresh_events[s.index] = ev
+        if self.comm_stream is not None and wait:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
 
     def zero_optimization_stage(self) -> int:
@@ -580,6 +812,7 @@ class ZeroEngine(nn.Module):
     def full_state_dict(self) -> dict:
         """Module state dict on CPU with every parameter materialised; stage 3 gathers one unit
         at a time (collective: call on every rank)."""
+        self._wait_refresh()
         names = self._pid_names()
         sd = {}
         in_units = set()
@@ -661,7 +894,7 @@ class ZeroEngine(nn.Module):
             opt = self.optimizer
             opt.load_state_dict({"step": shard["step"], "exp_avg": shard["exp_avg"], "exp_avg_sq": shard["exp_avg_sq"],
                                  "master": shard["master"], "param_groups": shard["param_groups"]})
-            self._refresh_params()
+            self._refresh_params(wait=True)
         else:
             self._load_full(ms["module"])
         self.global_steps = int(ms.get("global_steps", 0))
@@ -674,6 +907,7 @@ class ZeroEngine(nn.Module):
 
     @torch.no_grad()
     def _load_full(self, sd: dict) -> None:
+        self._wait_refresh()
         names = self._pid_names()
         for s in self.buckets:
             for p in s.params:

@@ -63,6 +63,10 @@ def load_checkpoint(path: str, model: torch.nn.Module, optimizer=None) -> dict:
     if optimizer is not None and state.get("optimizer") is not None:
         optimizer.load_state_dict(state["optimizer"])
     rt = getattr(model, "rt", None)
-    if rt is not None and state.get("dropout_step") is not None:
-        rt.rng.state[1:2].fill_(int(state["dropout_step"]))   # this rank's seed stays as it is
+    step = state.get("dropout_step")
+    if step is None and state.get("dropout_rng") is not None:
+        # checkpoints written before the key change kept the whole [seed, step] state
+        step = int(torch.as_tensor(state["dropout_rng"]).reshape(-1)[1])
+    if rt is not None and step is not None:
+        rt.rng.state[1:2].fill_(int(step))   # this rank's seed stays as it is
     return {"step": state["step"], "extra": state["extra"]}

@@ -63,7 +63,7 @@ def ddp_nosync_worker(rank, world, port, out_dir, impl):
     comm.destroy()
 
 
-def zero_worker(rank, world, port, out_dir, model_name, stage, n_steps, gas):
+def zero_worker(rank, world, port, out_dir, model_name, stage, n_steps, gas, clip=0.0, tag=""):
     from distributed_training_and_deepspeed_amd.comm import logger as clog
     from distributed_training_and_deepspeed_amd.parallel.zero import initialize
     comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
@@ -71,6 +71,7 @@ def zero_worker(rank, world, port, out_dir, model_name, stage, n_steps, gas):
     cfg = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": gas,
            "optimizer": {"type": "Adam", "params": {"lr": 1e-3}},
            "comms_logger": {"enabled": True, "prof_all": True},
+           "gradient_clipping": clip,
            "zero_optimization": {"stage": stage, "reduce_bucket_size": 50000}}
     eng, opt, _, _ = initialize(model=model, model_parameters=model.parameters(), config=cfg)
     ids, lab = _batches(model.cfg, rank, world, n_steps * gas)
@@ -87,7 +88,7 @@ def zero_worker(rank, world, port, out_dir, model_name, stage, n_steps, gas):
         torch.save({"shards": shards, "partition": eng.partition_numel(),
                     "comms": {k: {s: v[0] for s, v in d.items()} for k, d in clog.comms_logger.comms_dict.items()},
                     "layout": [(s.unit, s.numel, s.chunk, s.shard_off, s.shapes) for s in eng.segments]},
-                   os.path.join(out_dir, f"zero{stage}.pt"))
+                   os.path.join(out_dir, f"zero{stage}{tag}.pt"))
     comm.destroy()
 
 
@@ -138,4 +139,43 @@ def zero_ckpt_worker(rank, world, port, out_dir, stage, load_stage):
     if rank == 0:
         torch.save({"saved": saved, "loaded": loaded, "fa": fa, "fb": fb, "client": client, "tag": os.path.basename(path),
                     "gs": gs}, os.path.join(out_dir, f"ck{stage}{load_stage}.pt"))
+    comm.destroy()
+
+
+def zero_reshard_save_worker(rank, world, port, out_dir, stage):
+    """Train 2 steps at this world size and save a ZeRO checkpoint (+ the full module state)."""
+    from distributed_training_and_deepspeed_amd.parallel.zero import initialize
+    comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
+    model = build_model("tiny", impl="fused", seed=3)
+    cfg = {"optimizer": {"type": "Adam", "params": {"lr": 1e-3}},
+           "zero_optimization": {"stage": stage, "reduce_bucket_size": 50000}}
+    eng = initialize(model=model, model_parameters=model.parameters(), config=cfg)[0]
+    ids, lab = _batches(model.cfg, rank, world, 2)
+    for i in range(2):
+        eng.backward(eng(ids[i], labels=lab[i]).loss)
+        eng.step()
+    eng.save_checkpoint(os.path.join(out_dir, "ckpt"))
+    full = eng.full_state_dict()
+    if rank == 0:
+        torch.save(full, os.path.join(out_dir, "saved_full.pt"))
+    comm.destroy()
+
+
+def zero_reshard_load_worker(rank, world, port, out_dir, stage):
+    """A different world size loads the checkpoint (re-shard from the module state), then trains
+    one step: the loaded parameters must equal the saved ones, and every rank must agree."""
+    from distributed_training_and_deepspeed_amd.parallel.zero import initialize
+    comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
+    model = build_model("tiny", impl="fused", seed=99)
+    cfg = {"optimizer": {"type": "Adam", "params": {"lr": 1e-3}},
+           "zero_optimization": {"stage": stage, "reduce_bucket_size": 50000}}
+    eng = initialize(model=model, model_parameters=model.parameters(), config=cfg)[0]
+    eng.load_checkpoint(os.path.join(out_dir, "ckpt"))
+    loaded = eng.full_state_dict()
+    ids, lab = _batches(model.cfg, rank, world, 1, seed=11)
+    eng.backward(eng(ids[0], labels=lab[0]).loss)
+    eng.step()
+    after = eng.full_state_dict()
+    torch.save({"loaded": loaded, "after": after, "gs": eng.global_steps},
+               os.path.join(out_dir, f"reshard_r{rank}.pt"))
     comm.destroy()
