@@ -46,10 +46,11 @@ def test_captured_step_matches_eager():
         assert torch.equal(p, q), n
 
 
-@pytest.mark.parametrize("stage", [0, 1])
+@pytest.mark.parametrize("stage", [0, 1, 2, 3])
 def test_captured_zero_step_matches_eager(stage):
-    """zero_dp_training.py --graph: a replayed ZeRO stage-0/1 step (causal LM, fused Adam with
-    device-side step count, parameter refresh, RNG advance) equals the eager engine step."""
+    """zero_dp_training.py --graph: a replayed ZeRO step (causal LM, fused Adam with device-side
+    step count, parameter refresh, RNG advance; stage 2/3 landing regions and stage-3 gathered
+    units from the persistent arenas) equals the eager engine step."""
     import os
     from distributed_training_and_deepspeed_amd import comm
     from distributed_training_and_deepspeed_amd.parallel.zero import initialize
@@ -86,7 +87,8 @@ def test_captured_zero_step_matches_eager(stage):
         comm.destroy()
 
 
-def test_zero_script_graph_trains_like_eager():
+@pytest.mark.parametrize("stage", [0, 2, 3])
+def test_zero_script_graph_trains_like_eager(stage):
     """zero_dp_training.py end to end: --graph (default on one GPU) warms up on the first real
     batches and replays the rest -- the same steps on the same batches as --graph off."""
     import json
@@ -99,7 +101,7 @@ def test_zero_script_graph_trains_like_eager():
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(32000 + os.getpid() % 1000 + len(res)))
         out = subprocess.run([sys.executable, os.path.join(root, "zero_dp_training.py"), "--model-name", "causal-tiny",
                               "--training-steps", "8", "--seq-len", "128", "--batch-size", "2", "--quiet",
-                              "--no-memstats", "--graph", mode],
+                              "--no-memstats", "--graph", mode, "--stage", str(stage)],
                              env=env, capture_output=True, text=True, timeout=100, cwd=root)
         assert out.returncode == 0, out.stderr[-2000:]
         res[mode] = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])

@@ -143,3 +143,33 @@ def test_rccl_streams_are_high_priority(rccl_world1):
     dist.all_reduce(t, op=dist.ReduceOp.AVG)
     torch.cuda.synchronize()
     assert torch.all(t == 2.0)
+
+
+def test_ddp_deferred_finalize_no_sync_matches_inline(monkeypatch):
+    """World 1 with DTD_DEFER_FINALIZE=1 (bias / LN finalizes on the side stream): a no_sync
+    micro-step followed by a synced one accumulates exactly the gradients of the inline schedule
+    (the no_sync backward joins its side-stream writes before returning)."""
+    from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
+    from distributed_training_and_deepspeed_amd.models import build_model
+    from distributed_training_and_deepspeed_amd.ops.grad import _ASYNC
+    from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
+    ds = SyntheticLMDataset(build_model("tiny").cfg, 4 * 3, seq_len=128, seed=5)
+    ids = ds.input_ids.view(3, 4, 128).cuda()
+    lab = ds.labels.view(3, 4, 128).cuda()
+    grads = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DTD_DEFER_FINALIZE", mode)
+        model = build_model("tiny", dtype=torch.bfloat16, device="cuda", seed=3)
+        ddp = DistributedDataParallel(model)
+        assert ddp._defer_finalize == (mode == "1")
+        with ddp.no_sync():
+            ddp(ids[0], labels=lab[0]).loss.backward()
+        assert not _ASYNC.defer_finalize          # the no_sync backward closed the deferral window
+        ddp(ids[1], labels=lab[1]).loss.backward()
+        torch.cuda.synchronize()
+        grads[mode] = {n: p.main_grad.detach().clone() for n, p in model.named_parameters()}
+        with torch.no_grad():                     # a grad-free forward opens no deferral window
+            ddp(ids[2], labels=lab[2])
+        assert not _ASYNC.defer_finalize
+    for n in grads["0"]:
+        assert torch.equal(grads["0"][n], grads["1"][n]), n

@@ -49,11 +49,10 @@ def train(model_name, batch_size, training_steps, stage, opts):
     model = build_model(model_name, dtype=dtype, device=device, seed=0, impl=opts.impl)
 
     if opts.graph == "auto":  # multi-rank RCCL capture stays opt-in
-        opts.graph = "on" if (cuda and world_size == 1 and stage <= 1) else "off"
+        opts.graph = "on" if (cuda and world_size == 1) else "off"
+    # every stage is capturable: stage-2/3 gradient landing regions and stage-3 gathered units
+    # live in persistent ring arenas (parallel/zero.py _Arena), so replays reuse one address set
     graph = opts.graph == "on" and cuda
-    if graph and stage > 1:
-        raise SystemExit("--graph supports ZeRO stages 0 and 1 (stage 2/3 allocate gradient landing / "
-                         "gathered-parameter buffers per step)")
     ds_config = {
         "train_micro_batch_size_per_gpu": batch_size,
         "optimizer": {"type": "Adam", "params": {"lr": 0.00015}},
