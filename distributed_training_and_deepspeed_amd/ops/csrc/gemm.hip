@@ -949,198 +949,6 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
   if constexpr (DYN) sched_finish(g.sched, nwg, tid);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Persistent form, direct-store epilogue (EPI_STORE, optional bias; DTD_GEMM_VARIANT 3): the
-// K-step pipeline of gemm_bt_persistent, but a tile's epilogue neither goes through an LDS image
-// nor synchronises the workgroup.  Two packed bf16 fragments of adjacent 16-column blocks are
-// exchanged between lane rows by v_permlane16_swap, after which every lane holds 8 consecutive
-// columns of one row: 16 16-byte stores per wave (64-byte row segments).  The wave rows stay
-// staggered through the epilogue, so one row's epilogue runs beside the other row's MFMAs (the
-// last segment of the tile, or the first of the next).  The tile's bias (256 columns) comes into a
-// 512-byte LDS slot by LDS-DMA in the tile's last K-step, so no register-destination load sits in
-// the counted DMA pipeline (hipcc would drain it with vmcnt(0) at the first use).  Static
-// XCD-grouped tile order; K >= 128.
-constexpr int BIAS_LDS = LDS_BYTES;                 // 512-byte bias slot after the two K-step buffers
-constexpr int LDS3_BYTES = LDS_BYTES + 512;
-constexpr int DIRECT_STORES = 16;                   // vector-memory ops of one wave's epilogue
-
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  const bf16x2 v = {(bf16)a, (bf16)b};
-  return __builtin_bit_cast(uint32_t, v);
-}
-
-// bf16 store of accumulator quadrant (qm, column blocks nb, nb + 1) of one wave: 4 x 16 rows;
-// bq[0] / bq[1]: the bias of blocks nb / nb + 1 at the lane's 4 columns
-template <bool BIAS>
-__device__ __forceinline__ void store_quadrant(const f32x4 (&acc)[8][4], int qm, int nb, const bf16x4 (&bq)[2],
-                                               bf16* __restrict__ c, int ldc, int m0, int n0, int wm, int wn, int li,
-                                               int lq) {
-  const int ecol = (lq & 1) * 16 + (lq >> 1) * 8;
-  bf16* base = c + (size_t)(m0 + wm * 128 + qm * 64 + li) * ldc + n0 + wn * 64 + nb * 16 + ecol;
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    f32x4 X = acc[qm * 4 + mi][nb], Y = acc[qm * 4 + mi][nb + 1];
-    if constexpr (BIAS) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        X[k] += (float)bq[0][k];
-        Y[k] += (float)bq[1][k];
-      }
-    }
-    const uint32_t x0 = pack_bf16x2(X[0], X[1]), x1 = pack_bf16x2(X[2], X[3]);
-    const uint32_t y0 = pack_bf16x2(Y[0], Y[1]), y1 = pack_bf16x2(Y[2], Y[3]);
-    const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-    const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
-    *reinterpret_cast<u32x4*>(base + (size_t)mi * 16 * ldc) = v;
-  }
-}
-
-template <bool BIAS>
-__global__ void __launch_bounds__(512, 2) gemm_bt_pers3(GemmArgs g) {
-  __shared__ __attribute__((aligned(1024))) char smem[LDS3_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int li = lane & 15, lq = lane >> 4, sw = li & 7;
-  const int wm = w >> 2, wn = w & 3;
-  const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn;
-  const int nk = g.K / BK;   // >= 2 (host check)
-  const int nwg = gridDim.x, x = blockIdx.x % 8, l = blockIdx.x / 8, per = nwg / 8;
-  const int q = ntiles / 8, r = ntiles % 8;
-  const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-  const int end = beg + q + (x < r ? 1 : 0);
-  int t = beg + l;
-  if (t >= end) return;
-  int m0, n0;
-  tile_of(t, ntn, m0, n0);
-  const StageOffs so = stage_offsets(w, lane, g.lda, g.ldb);
-  auto rsa = uniform_rsrc(g.a + (size_t)m0 * g.lda), rsb = uniform_rsrc(g.b + (size_t)n0 * g.ldb);
-  const auto rbias = uniform_rsrc(BIAS ? (const void*)g.bias : (const void*)g.a);
-  stage<0>(so, rsa, rsb, smem, 0);
-  stage<1>(so, rsa, rsb, smem, 0);
-  stage<2>(so, rsa, rsb, smem, 0);
-  stage<3>(so, rsa, rsb, smem, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (__builtin_amdgcn_readfirstlane(wm) == 1) bar();   // stagger wave row 1
-
-  const int arow = (wm * 128 + li) * 128;
-  const int brow = A_BYTES + (wn * 64 + li) * 128;
-  const int ch0 = ((0 * 4 + lq) ^ sw) * 16, ch1 = ((1 * 4 + lq) ^ sw) * 16;
-  constexpr int BL = BIAS ? 1 : 0;
-  // counted waits (a phase retires the quarter DMA of two phases ago; younger are the ops issued
-  // since): first K-step after an epilogue, phases 0-1: 2 + 16 stores + 2; the last K-step,
-  // phases 0-1: + the bias DMA; the very last K-step (nothing staged): 2 + bias, bias, 0, 0
-  constexpr int WAIT_EPI = 4 + DIRECT_STORES;
-
-  bf16x8 af[4][2], b0[2][2], b1[2][2];
-  f32x4 acc[8][4];
-  int buf = 0;
-  bool after_epi = false;
-  while (true) {
-    const int tn = t + per;
-    const bool has_next = tn < end;
-    int m1 = 0, n1 = 0;
-    if (has_next) tile_of(tn, ntn, m1, n1);
-    const auto rsa1 = uniform_rsrc(g.a + (size_t)m1 * g.lda), rsb1 = uniform_rsrc(g.b + (size_t)n1 * g.ldb);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int kt = 0; kt < nk; ++kt) {
-      const char* cur = smem + buf * TILE_BYTES;
-      char* nxt = smem + (buf ^ 1) * TILE_BYTES;
-      buf ^= 1;
-      const bool more_here = kt + 1 < nk;
-      const bool more = more_here || has_next;
-      const auto sra = more_here ? rsa : rsa1, srb = more_here ? rsb : rsb1;
-      const int skt = more_here ? kt + 1 : 0;
-      const bool first = kt == 0 && after_epi;
-      const bool lastk = !more_here;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        if (p == 0 || p == 2) {
-          const int qm = p == 0 ? 0 : 1;
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) {
-            const char* rr = cur + arow + (qm * 4 + mi) * 16 * 128;
-            af[mi][0] = *reinterpret_cast<const bf16x8*>(rr + ch0);
-            af[mi][1] = *reinterpret_cast<const bf16x8*>(rr + ch1);
-          }
-        }
-        if (p == 0 || p == 1) {
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni) {
-            const char* rr = cur + brow + (p * 2 + ni) * 16 * 128;
-            bf16x8 x0 = *reinterpret_cast<const bf16x8*>(rr + ch0);
-            bf16x8 x1 = *reinterpret_cast<const bf16x8*>(rr + ch1);
-            if (p == 0) { b0[ni][0] = x0; b0[ni][1] = x1; } else { b1[ni][0] = x0; b1[ni][1] = x1; }
-          }
-        }
-        if constexpr (BIAS) {
-          if (lastk && p == 0)   // this tile's 256 bias values -> LDS (every wave: 256 of the 512 B)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias, (lds_void*)(smem + BIAS_LDS + (w & 1) * 256), 4,
-                                                      (n0 + (w & 1) * 128) * 2 + lane * 4, 0, 0, 0);
-        }
-        if (more) {
-          if (p == 0) stage<0>(so, sra, srb, nxt, skt);
-          if (p == 1) stage<1>(so, sra, srb, nxt, skt);
-          if (p == 2) stage<2>(so, sra, srb, nxt, skt);
-          if (p == 3) stage<3>(so, sra, srb, nxt, skt);
-          if (p < 2 && first) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WAIT_EPI) : "memory");
-          else if (p < 2 && lastk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 + BL) : "memory");
-          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else if (p == 0) {
-          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 + BL) : "memory");
-        } else if (p == 1) {
-          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(BL) : "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        bar();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        const int qm = (p == 2 || p == 3) ? 1 : 0;
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-              const bf16x8 bb = (p == 1 || p == 2) ? b1[ni][ks] : b0[ni][ks];
-              const int nn = ((p == 1 || p == 2) ? 2 : 0) + ni;
-              acc[qm * 4 + mi][nn] = mfma16(bb, af[mi][ks], acc[qm * 4 + mi][nn]);
-            }
-        __builtin_amdgcn_s_setprio(0);
-        bar();
-      }
-    }
-    // ---- epilogue: registers -> global, no LDS image, no workgroup barrier (the bias DMA of
-    //      this tile was retired by the last K-step's phase-2 wait, which every wave passed)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int eqm = e >> 1, enb = (e & 1) * 2;
-      bf16x4 bq[2] = {};
-      if constexpr (BIAS) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          bq[j] = *reinterpret_cast<const bf16x4*>(smem + BIAS_LDS + (wn * 64 + (enb + j) * 16 + 4 * lq) * 2);
-      }
-      store_quadrant<BIAS>(acc, eqm, enb, bq, g.c, g.ldc, m0, n0, wm, wn, li, lq);
-    }
-    after_epi = true;
-    if (!has_next) break;
-    t = tn;
-    m0 = m1;
-    n0 = n1;
-    rsa = rsa1;
-    rsb = rsb1;
-  }
-  if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
-}
-
 // W [rows][cols] -> WT [cols][rows], bf16, 64 x 64 tiles through LDS (padded rows).  Vector form
 // (rows, cols multiples of 8): 16-byte global loads and stores; otherwise element-wise.
 __global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
@@ -1248,13 +1056,6 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
   GemmArgs g{(const bf16*)a, (const bf16*)b, (bf16*)c, (bf16*)c2, (const bf16*)u, (const bf16*)bias, part,
              M, N, K, lda, ldb, ldc, ldu, g_stamps, nullptr};
   const int ntiles = (M / BM) * (N / BN);
-  if (gemm_variant() == 3 && epi == EPI_STORE && K >= 2 * BK) {
-    const int cus = num_cus() / 8 * 8;
-    const int nwg = ntiles >= cus ? cus : (ntiles + 7) / 8 * 8;
-    if (bias) hipLaunchKernelGGL((gemm_bt_pers3<true>), dim3(nwg), dim3(512), 0, s, g);
-    else hipLaunchKernelGGL((gemm_bt_pers3<false>), dim3(nwg), dim3(512), 0, s, g);
-    DTD_LAUNCH_CHECK();
-  }
   if (gemm_variant() >= 1) {
     const int cus = num_cus() / 8 * 8;
     const int nwg = ntiles >= cus ? cus : (ntiles + 7) / 8 * 8;

@@ -1,6 +1,7 @@
 #!/usr/bin/env python
-"""Persistent GEMM v2 (deferred quadrant epilogue, ops/csrc/gemm.hip gemm_bt_pers2) vs v1 (LDS-image
-epilogue) vs hipBLASLt, C = A B^T (+ bias), bf16, at the BERT-base b256 plain projection shapes.
+"""A GEMM kernel form (DTD_GEMM_VARIANT = VNEW, default 4) vs the production persistent form v1 vs
+hipBLASLt, C = A B^T (+ bias), bf16, at the BERT-base b256 plain projection shapes.  The round-3
+experimental forms live in scripts/experiments/gemm_variants_r3.hip (paste into gemm.hip to rerun).
 
 1. correctness: v2 against an fp32 reference on several shapes (1 tile per workgroup, several,
    uneven XCD groups, with / without bias);
@@ -16,6 +17,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_training_and_deepspeed_amd.ops import _lib  # noqa: E402
 from distributed_training_and_deepspeed_amd.ops import gemm as G  # noqa: E402
+
+
+VNEW = int(os.environ.get("VNEW", "4"))   # the variant compared against v1 (the "v2" columns)
 
 
 def setv(v):
@@ -40,7 +44,7 @@ def check():
             if bias is not None:
                 ref += bias.float()
             c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-            run(a, b, c, bias, 3)
+            run(a, b, c, bias, VNEW)
             torch.cuda.synchronize()
             err = ((c.float() - ref).norm() / ref.norm()).item()
             nan = bool(torch.isnan(c).any())
@@ -77,7 +81,7 @@ def main():
         bias = torch.rand(N, device="cuda", dtype=torch.bfloat16) if with_bias else None
         c = torch.empty(T, N, device="cuda", dtype=torch.bfloat16)
         fns = {"hipblaslt": (lambda: torch.nn.functional.linear(a, b, bias)),
-               "v1": (lambda: run(a, b, c, bias, 1)), "v2": (lambda: run(a, b, c, bias, 3))}
+               "v1": (lambda: run(a, b, c, bias, 1)), "v2": (lambda: run(a, b, c, bias, VNEW))}
         for f in fns.values():
             f()
         torch.cuda.synchronize()

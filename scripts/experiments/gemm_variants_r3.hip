@@ -1,0 +1,559 @@
+// Round-3 GEMM main-loop experiments (NOT compiled into the library; kept for reproducibility).
+// Each was built into ops/csrc/gemm.hip as a DTD_GEMM_VARIANT, checked against an fp32 reference
+// and timed against the production persistent kernel (v1) and hipBLASLt with
+// scripts/bench_gemm_v2.py at the BERT-base b256 projection shapes.  All three lost to v1:
+//  * variant 3, direct-store epilogue (no LDS image, v_permlane16_swap 16-byte row pieces, wave
+//    rows stay staggered through the epilogue): 0.95-0.99x v1
+//    (profiles/r3_gemm_direct_store_epilogue.jsonl) -- the epilogue is not the limiter;
+//  * variant 4, four waves / one per SIMD, 128x128 per wave with 256 AGPR accumulators, own LDS
+//    reads interleaved between MFMAs, one barrier per K-step: 0.65-0.80x v1
+//    (profiles/r3_gemm_w4_experiment.jsonl);
+//  * variant 5, deep prefetch (each K-step quarter restaged as soon as it is consumed, two K-steps
+//    ahead of its readers): 0.75-0.82x v1 (profiles/r3_gemm_deep_prefetch_experiment.jsonl).
+// They need gemm.hip's helpers (stage, stage_offsets, uniform_rsrc, bar, mfma16, tile_of, ...).
+// ---------------------------------------------------------------------------------------------
+// Persistent form, direct-store epilogue (EPI_STORE, optional bias; DTD_GEMM_VARIANT 3): the
+// K-step pipeline of gemm_bt_persistent, but a tile's epilogue neither goes through an LDS image
+// nor synchronises the workgroup.  Two packed bf16 fragments of adjacent 16-column blocks are
+// exchanged between lane rows by v_permlane16_swap, after which every lane holds 8 consecutive
+// columns of one row: 16 16-byte stores per wave (64-byte row segments).  The wave rows stay
+// staggered through the epilogue, so one row's epilogue runs beside the other row's MFMAs (the
+// last segment of the tile, or the first of the next).  The tile's bias (256 columns) comes into a
+// 512-byte LDS slot by LDS-DMA in the tile's last K-step, so no register-destination load sits in
+// the counted DMA pipeline (hipcc would drain it with vmcnt(0) at the first use).  Static
+// XCD-grouped tile order; K >= 128.
+constexpr int BIAS_LDS = LDS_BYTES;                 // 512-byte bias slot after the two K-step buffers
+constexpr int LDS3_BYTES = LDS_BYTES + 512;
+constexpr int DIRECT_STORES = 16;                   // vector-memory ops of one wave's epilogue
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const bf16x2 v = {(bf16)a, (bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// bf16 store of accumulator quadrant (qm, column blocks nb, nb + 1) of one wave: 4 x 16 rows;
+// bq[0] / bq[1]: the bias of blocks nb / nb + 1 at the lane's 4 columns
+template <bool BIAS>
+__device__ __forceinline__ void store_quadrant(const f32x4 (&acc)[8][4], int qm, int nb, const bf16x4 (&bq)[2],
+                                               bf16* __restrict__ c, int ldc, int m0, int n0, int wm, int wn, int li,
+                                               int lq) {
+  const int ecol = (lq & 1) * 16 + (lq >> 1) * 8;
+  bf16* base = c + (size_t)(m0 + wm * 128 + qm * 64 + li) * ldc + n0 + wn * 64 + nb * 16 + ecol;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    f32x4 X = acc[qm * 4 + mi][nb], Y = acc[qm * 4 + mi][nb + 1];
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        X[k] += (float)bq[0][k];
+        Y[k] += (float)bq[1][k];
+      }
+    }
+    const uint32_t x0 = pack_bf16x2(X[0], X[1]), x1 = pack_bf16x2(X[2], X[3]);
+    const uint32_t y0 = pack_bf16x2(Y[0], Y[1]), y1 = pack_bf16x2(Y[2], Y[3]);
+    const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
+    *reinterpret_cast<u32x4*>(base + (size_t)mi * 16 * ldc) = v;
+  }
+}
+
+template <bool BIAS>
+__global__ void __launch_bounds__(512, 2) gemm_bt_pers3(GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS3_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4, sw = li & 7;
+  const int wm = w >> 2, wn = w & 3;
+  const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn;
+  const int nk = g.K / BK;   // >= 2 (host check)
+  const int nwg = gridDim.x, x = blockIdx.x % 8, l = blockIdx.x / 8, per = nwg / 8;
+  const int q = ntiles / 8, r = ntiles % 8;
+  const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const int end = beg + q + (x < r ? 1 : 0);
+  int t = beg + l;
+  if (t >= end) return;
+  int m0, n0;
+  tile_of(t, ntn, m0, n0);
+  const StageOffs so = stage_offsets(w, lane, g.lda, g.ldb);
+  auto rsa = uniform_rsrc(g.a + (size_t)m0 * g.lda), rsb = uniform_rsrc(g.b + (size_t)n0 * g.ldb);
+  const auto rbias = uniform_rsrc(BIAS ? (const void*)g.bias : (const void*)g.a);
+  stage<0>(so, rsa, rsb, smem, 0);
+  stage<1>(so, rsa, rsb, smem, 0);
+  stage<2>(so, rsa, rsb, smem, 0);
+  stage<3>(so, rsa, rsb, smem, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(wm) == 1) bar();   // stagger wave row 1
+
+  const int arow = (wm * 128 + li) * 128;
+  const int brow = A_BYTES + (wn * 64 + li) * 128;
+  const int ch0 = ((0 * 4 + lq) ^ sw) * 16, ch1 = ((1 * 4 + lq) ^ sw) * 16;
+  constexpr int BL = BIAS ? 1 : 0;
+  // counted waits (a phase retires the quarter DMA of two phases ago; younger are the ops issued
+  // since): first K-step after an epilogue, phases 0-1: 2 + 16 stores + 2; the last K-step,
+  // phases 0-1: + the bias DMA; the very last K-step (nothing staged): 2 + bias, bias, 0, 0
+  constexpr int WAIT_EPI = 4 + DIRECT_STORES;
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  f32x4 acc[8][4];
+  int buf = 0;
+  bool after_epi = false;
+  while (true) {
+    const int tn = t + per;
+    const bool has_next = tn < end;
+    int m1 = 0, n1 = 0;
+    if (has_next) tile_of(tn, ntn, m1, n1);
+    const auto rsa1 = uniform_rsrc(g.a + (size_t)m1 * g.lda), rsb1 = uniform_rsrc(g.b + (size_t)n1 * g.ldb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* cur = smem + buf * TILE_BYTES;
+      char* nxt = smem + (buf ^ 1) * TILE_BYTES;
+      buf ^= 1;
+      const bool more_here = kt + 1 < nk;
+      const bool more = more_here || has_next;
+      const auto sra = more_here ? rsa : rsa1, srb = more_here ? rsb : rsb1;
+      const int skt = more_here ? kt + 1 : 0;
+      const bool first = kt == 0 && after_epi;
+      const bool lastk = !more_here;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (p == 0 || p == 2) {
+          const int qm = p == 0 ? 0 : 1;
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) {
+            const char* rr = cur + arow + (qm * 4 + mi) * 16 * 128;
+            af[mi][0] = *reinterpret_cast<const bf16x8*>(rr + ch0);
+            af[mi][1] = *reinterpret_cast<const bf16x8*>(rr + ch1);
+          }
+        }
+        if (p == 0 || p == 1) {
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) {
+            const char* rr = cur + brow + (p * 2 + ni) * 16 * 128;
+            bf16x8 x0 = *reinterpret_cast<const bf16x8*>(rr + ch0);
+            bf16x8 x1 = *reinterpret_cast<const bf16x8*>(rr + ch1);
+            if (p == 0) { b0[ni][0] = x0; b0[ni][1] = x1; } else { b1[ni][0] = x0; b1[ni][1] = x1; }
+          }
+        }
+        if constexpr (BIAS) {
+          if (lastk && p == 0)   // this tile's 256 bias values -> LDS (every wave: 256 of the 512 B)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias, (lds_void*)(smem + BIAS_LDS + (w & 1) * 256), 4,
+                                                      (n0 + (w & 1) * 128) * 2 + lane * 4, 0, 0, 0);
+        }
+        if (more) {
+          if (p == 0) stage<0>(so, sra, srb, nxt, skt);
+          if (p == 1) stage<1>(so, sra, srb, nxt, skt);
+          if (p == 2) stage<2>(so, sra, srb, nxt, skt);
+          if (p == 3) stage<3>(so, sra, srb, nxt, skt);
+          if (p < 2 && first) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WAIT_EPI) : "memory");
+          else if (p < 2 && lastk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 + BL) : "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else if (p == 0) {
+          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 + BL) : "memory");
+        } else if (p == 1) {
+          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(BL) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        const int qm = (p == 2 || p == 3) ? 1 : 0;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+              const bf16x8 bb = (p == 1 || p == 2) ? b1[ni][ks] : b0[ni][ks];
+              const int nn = ((p == 1 || p == 2) ? 2 : 0) + ni;
+              acc[qm * 4 + mi][nn] = mfma16(bb, af[mi][ks], acc[qm * 4 + mi][nn]);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        bar();
+      }
+    }
+    // ---- epilogue: registers -> global, no LDS image, no workgroup barrier (the bias DMA of
+    //      this tile was retired by the last K-step's phase-2 wait, which every wave passed)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int eqm = e >> 1, enb = (e & 1) * 2;
+      bf16x4 bq[2] = {};
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bq[j] = *reinterpret_cast<const bf16x4*>(smem + BIAS_LDS + (wn * 64 + (enb + j) * 16 + 4 * lq) * 2);
+      }
+      store_quadrant<BIAS>(acc, eqm, enb, bq, g.c, g.ldc, m0, n0, wm, wn, li, lq);
+    }
+    after_epi = true;
+    if (!has_next) break;
+    t = tn;
+    m0 = m1;
+    n0 = n1;
+    rsa = rsa1;
+    rsb = rsb1;
+  }
+  if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deep-prefetch persistent form (DTD_GEMM_VARIANT 5; EPI_STORE, optional bias): the 8-wave
+// 4-phase main loop and direct-store epilogue of gemm_bt_pers3, but every quarter of a K-step
+// buffer is restaged the moment the current K-step has consumed it: A-lo and B-lo are read only in
+// phase 0, B-hi in phase 1, A-hi in phase 2, so K-step i + 2's quarters H0 + H1 go out in phase 1
+// of K-step i, H2 in phase 2, H3 in phase 3 -- two K-steps (8 phases) ahead of their readers,
+// instead of the 2 phases of the other forms.  Per wave and K-step: phase 0 issues nothing (the
+// tile's bias DMA, first K-step only), phase 1 four DMAs, phases 2 and 3 two each.  Waits: phase 3
+// retires H0 + H1 of K-step i + 1 (12 younger ops), phase 0 H2 (10), phase 1 H3 (12), phase 2
+// none; + 16 after an epilogue in between, + 1 for the bias DMA; the last two K-steps of the
+// stream drain with vmcnt(0).  K >= 128.
+template <bool BIAS>
+__global__ void __launch_bounds__(512, 2) gemm_bt_pers5(GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + 1024];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4, sw = li & 7;
+  const int wm = w >> 2, wn = w & 3;
+  const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn;
+  const int nk = g.K / BK;   // >= 2 (host check)
+  const int nwg = gridDim.x, x = blockIdx.x % 8, l = blockIdx.x / 8, per = nwg / 8;
+  const int q = ntiles / 8, r = ntiles % 8;
+  const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const int end = beg + q + (x < r ? 1 : 0);
+  int t = beg + l;
+  if (t >= end) return;
+  const int ntl = (end - t + per - 1) / per;
+  const int G = ntl * nk;   // K-steps of this workgroup's stream
+  int m0, n0;
+  tile_of(t, ntn, m0, n0);
+  const StageOffs so = stage_offsets(w, lane, g.lda, g.ldb);
+  auto panel_a = [&](int tile) { int a, b; tile_of(tile, ntn, a, b); return uniform_rsrc(g.a + (size_t)a * g.lda); };
+  auto panel_b = [&](int tile) { int a, b; tile_of(tile, ntn, a, b); return uniform_rsrc(g.b + (size_t)b * g.ldb); };
+  auto rsa = panel_a(t), rsb = panel_b(t);
+  const int t1 = t + per < end ? t + per : t;
+  auto rsa1 = panel_a(t1), rsb1 = panel_b(t1);
+  const auto rbias = uniform_rsrc(BIAS ? (const void*)g.bias : (const void*)g.a);
+  // prologue: K-steps 0 and 1 (both of the first tile), quarters in order
+  stage<0>(so, rsa, rsb, smem, 0);
+  stage<1>(so, rsa, rsb, smem, 0);
+  stage<2>(so, rsa, rsb, smem, 0);
+  stage<3>(so, rsa, rsb, smem, 0);
+  stage<0>(so, rsa, rsb, smem + TILE_BYTES, 1);
+  stage<1>(so, rsa, rsb, smem + TILE_BYTES, 1);
+  stage<2>(so, rsa, rsb, smem + TILE_BYTES, 1);
+  stage<3>(so, rsa, rsb, smem + TILE_BYTES, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(wm) == 1) bar();   // stagger wave row 1
+
+  const int arow = (wm * 128 + li) * 128;
+  const int brow = A_BYTES + (wn * 64 + li) * 128;
+  const int ch0 = ((0 * 4 + lq) ^ sw) * 16, ch1 = ((1 * 4 + lq) ^ sw) * 16;
+  constexpr int BL = BIAS ? 1 : 0;
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  f32x4 acc[8][4];
+  int it = 0;
+  for (int i = 0; i < G; ++i) {
+    const int k = i - it * nk;              // K-step within the tile
+    const char* cur = smem + (i & 1) * TILE_BYTES;
+    char* cw = smem + (i & 1) * TILE_BYTES;   // K-step i + 2 lands in this same buffer
+    const bool st2 = i + 2 < G;             // K-step i + 2 exists
+    const bool nxt2 = k + 2 >= nk;          // ... and belongs to the next tile
+    const auto sra = nxt2 ? rsa1 : rsa, srb = nxt2 ? rsb1 : rsb;
+    const int sk = nxt2 ? k + 2 - nk : k + 2;
+    const bool tail = i + 2 >= G;
+    const bool e1 = k == 0 && it > 0;       // an epilogue ran right before this K-step
+    const bool e2 = k == 1 && it > 0;       // ... right before the previous one
+    const bool b1k = BIAS && (k == 0);      // this K-step issues the bias DMA (phase 0)
+    const bool b2k = BIAS && (k == 1);      // the previous one did
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p == 0 || p == 2) {
+        const int qm = p == 0 ? 0 : 1;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const char* rr = cur + arow + (qm * 4 + mi) * 16 * 128;
+          af[mi][0] = *reinterpret_cast<const bf16x8*>(rr + ch0);
+          af[mi][1] = *reinterpret_cast<const bf16x8*>(rr + ch1);
+        }
+      }
+      if (p == 0 || p == 1) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const char* rr = cur + brow + (p * 2 + ni) * 16 * 128;
+          bf16x8 x0 = *reinterpret_cast<const bf16x8*>(rr + ch0);
+          bf16x8 x1 = *reinterpret_cast<const bf16x8*>(rr + ch1);
+          if (p == 0) { b0[ni][0] = x0; b0[ni][1] = x1; } else { b1[ni][0] = x0; b1[ni][1] = x1; }
+        }
+      }
+      if constexpr (BIAS) {
+        if (p == 0 && k == 0)   // this tile's 256 bias values -> its LDS slot (tile parity)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias, (lds_void*)(smem + LDS_BYTES + (it & 1) * 512 + (w & 1) * 256),
+                                                    4, (n0 + (w & 1) * 128) * 2 + lane * 4, 0, 0, 0);
+      }
+      if (st2) {   // restage the quarters this K-step has consumed with K-step i + 2
+        if (p == 1) { stage<0>(so, sra, srb, cw, sk); stage<1>(so, sra, srb, cw, sk); }
+        if (p == 2) stage<2>(so, sra, srb, cw, sk);
+        if (p == 3) stage<3>(so, sra, srb, cw, sk);
+      }
+      if (tail) {
+        if (p != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (p == 0) {
+        if (e1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(10 + DIRECT_STORES + BL) : "memory");
+        else if (e2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(10 + DIRECT_STORES + BL) : "memory");
+        else if (b1k || b2k) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(10 + BL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      } else if (p == 1) {
+        if (e1 || e2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(12 + DIRECT_STORES + BL) : "memory");
+        else if (b1k || b2k) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(12 + BL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      } else if (p == 3) {
+        if (e1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(12 + DIRECT_STORES + BL) : "memory");
+        else if (b1k) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(12 + BL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      }
+      bar();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      const int qm = (p == 2 || p == 3) ? 1 : 0;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            const bf16x8 bb = (p == 1 || p == 2) ? b1[ni][ks] : b0[ni][ks];
+            const int nn = ((p == 1 || p == 2) ? 2 : 0) + ni;
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            acc[qm * 4 + mi][nn] = mfma16(bb, af[mi][ks], (k == 0 && ks == 0) ? z : acc[qm * 4 + mi][nn]);
+          }
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+    }
+    if (k == nk - 1) {   // tile done: direct-store epilogue (bias retired at its 2nd K-step's phase 3)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int eqm = e >> 1, enb = (e & 1) * 2;
+        bf16x4 bq[2] = {};
+        if constexpr (BIAS) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            bq[j] = *reinterpret_cast<const bf16x4*>(smem + LDS_BYTES + (it & 1) * 512 +
+                                                     (wn * 64 + (enb + j) * 16 + 4 * lq) * 2);
+        }
+        store_quadrant<BIAS>(acc, eqm, enb, bq, g.c, g.ldc, m0, n0, wm, wn, li, lq);
+      }
+      ++it;
+      t += per;
+      tile_of(t < end ? t : beg, ntn, m0, n0);
+      rsa = rsa1;
+      rsb = rsb1;
+      const int tn = t + per < end ? t + per : t;
+      rsa1 = panel_a(tn);
+      rsb1 = panel_b(tn);
+    }
+  }
+  if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
+}
+
+// ---------------------------------------------------------------------------------------------
+// W4 form (DTD_GEMM_VARIANT 4; EPI_STORE, optional bias): FOUR waves, one per SIMD, each owning a
+// 128 x 128 quarter of the 256 x 256 tile -- 256 fp32 accumulators per lane in AGPRs (a single
+// wave per SIMD may use the whole 512-entry register file), so a K-step costs each wave 32 LDS
+// fragment reads for 128 MFMAs (0.25 reads per MFMA; the 8-wave 128 x 64 split needs 0.375).
+// With no partner wave on the SIMD, each wave hides its own LDS reads and LDS-DMA issue between
+// its MFMAs (sched_group_barrier interleave) instead of alternating read / MFMA segments with a
+// partner across 8 barriers per K-step: ONE barrier per K-step.
+//   K-step g (buffer g & 1): part 1 = MFMAs of k-half 0 (fragments X) while reading k-half 1 (Y);
+//   wait for the DMA of K-step g + 1; barrier; part 2 = MFMAs of k-half 1 (Y) while reading
+//   k-half 0 of K-step g + 1 (X) and issuing the DMA of K-step g + 2 into buffer g & 1.
+// The K-step stream runs across the workgroup's tiles (persistent, XCD-grouped static order);
+// a tile's epilogue (bf16 + bias, v_permlane16_swap into 16-byte row pieces, direct stores) sits
+// between its last K-step and the next tile's first, whose MFMAs start from C = 0.  The bias of a
+// tile reaches a 512-byte LDS slot (tile parity) by LDS-DMA in its first K-step.  K >= 128.
+constexpr int W4_LDS = LDS_BYTES + 1024;
+constexpr int W4_STORES = 32;   // vector-memory ops of one wave's epilogue
+
+struct W4Ctx {
+  int voff;        // per-lane DMA source offset (row L/8 of an 8-row piece, swizzled chunk)
+  int abase, bbase;   // per-lane fragment read offsets within a K-step buffer (chunk of k-half 0)
+  int kh1;         // byte delta from the k-half 0 chunk to the k-half 1 chunk
+  int w, wm, wn, li, lq, lane;
+};
+
+// the 16 DMA pieces of one wave for K-step `kk` of the tile whose operand panel is `rs`
+__device__ __forceinline__ void w4_stage(const W4Ctx& C, __amdgpu_buffer_rsrc_t rs, int ld, char* buf, int kk,
+                                         int i0, int i1) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i < i0 || i >= i1) continue;
+    const int j = C.w * 16 + i;   // 8-row piece of the [A; B] 512-row image
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(buf + j * 1024), 16, C.voff, kk * BK * 2 + i * 16 * ld, 0,
+                                              0);
+  }
+}
+
+template <bool BIAS>
+__device__ __forceinline__ void w4_epilogue(const f32x4 (&acc)[8][8], const char* bias_lds, bf16* __restrict__ c,
+                                            int ldc, int m0, int n0, const W4Ctx& C) {
+  const int ecol = (C.lq & 1) * 16 + (C.lq >> 1) * 8;
+  bf16* base = c + (size_t)(m0 + C.wm * 128 + C.li) * ldc + n0 + C.wn * 128 + ecol;
+#pragma unroll
+  for (int nb = 0; nb < 8; nb += 2) {
+    bf16x4 bx = {}, by = {};
+    if constexpr (BIAS) {
+      bx = *reinterpret_cast<const bf16x4*>(bias_lds + (C.wn * 128 + nb * 16 + 4 * C.lq) * 2);
+      by = *reinterpret_cast<const bf16x4*>(bias_lds + (C.wn * 128 + (nb + 1) * 16 + 4 * C.lq) * 2);
+    }
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) {
+      f32x4 X = acc[mb][nb], Y = acc[mb][nb + 1];
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          X[k] += (float)bx[k];
+          Y[k] += (float)by[k];
+        }
+      }
+      const uint32_t x0 = pack_bf16x2(X[0], X[1]), x1 = pack_bf16x2(X[2], X[3]);
+      const uint32_t y0 = pack_bf16x2(Y[0], Y[1]), y1 = pack_bf16x2(Y[2], Y[3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
+      *reinterpret_cast<u32x4*>(base + (size_t)mb * 16 * ldc + nb * 16) = v;
+    }
+  }
+}
+
+// fragments of one k-half: A[mb] (8) and B[nb] (8) of the wave's quarter
+__device__ __forceinline__ void w4_read(const char* buf, const W4Ctx& C, int kh, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+  const char* pa = buf + C.abase + kh * C.kh1;
+  const char* pb = buf + C.bbase + kh * C.kh1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa[i] = *reinterpret_cast<const bf16x8*>(pa + i * 2048);
+    fb[i] = *reinterpret_cast<const bf16x8*>(pb + i * 2048);
+  }
+}
+
+template <bool ZERO>
+__device__ __forceinline__ void w4_mfma(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fb[nb], fa[mb], ZERO ? z : acc[mb][nb]);
+}
+
+// interleave: per group, `nds` LDS reads, `nvm` VMEM issues, `nmf` MFMAs
+__device__ __forceinline__ void w4_sched(int dummy) { (void)dummy; }
+#define DTD_W4_SCHED(GROUPS, NDS, NVM, NMF)                                  \
+  do {                                                                       \
+    _Pragma("unroll") for (int _g = 0; _g < (GROUPS); ++_g) {                \
+      if ((NDS) > 0) __builtin_amdgcn_sched_group_barrier(0x100, (NDS), 0);  \
+      if ((NVM) > 0) __builtin_amdgcn_sched_group_barrier(0x020, (NVM), 0);  \
+      __builtin_amdgcn_sched_group_barrier(0x008, (NMF), 0);                 \
+    }                                                                        \
+  } while (0)
+
+template <bool BIAS>
+__global__ void __launch_bounds__(256, 1) gemm_bt_w4(GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) char smem[W4_LDS];
+  // wave index through readfirstlane: provably uniform, so everything derived from it (operand,
+  // leading dimension, DMA soffsets) stays in SGPRs -- no waterfall loops around the DMA
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  W4Ctx C;
+  C.w = w; C.wm = w >> 1; C.wn = w & 1; C.li = lane & 15; C.lq = lane >> 4; C.lane = lane;
+  const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn;
+  const int nk = g.K / BK;   // >= 2 (host check)
+  const int nwg = gridDim.x, x = blockIdx.x % 8, l = blockIdx.x / 8, per = nwg / 8;
+  const int q = ntiles / 8, r = ntiles % 8;
+  const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const int end = beg + q + (x < r ? 1 : 0);
+  int t = beg + l;
+  if (t >= end) return;
+  const int ntl = (end - t + per - 1) / per;   // tiles of this workgroup
+  const int ng = ntl * nk;                     // its K-steps
+  // DMA: waves 0-1 stage A rows, 2-3 B rows; lane L -> row L/8 of an 8-row piece, chunk slot
+  // L%8 <- global chunk (L%8) ^ (L/8) (the involutive swizzle of the fragment reads)
+  const bool isb = w >= 2;
+  const int ld = isb ? g.ldb : g.lda;
+  C.voff = ((((w & 1) * 16 * 8) + (lane >> 3)) * ld + (((lane & 7) ^ (lane >> 3)) * 8)) * 2;
+  const int sw = C.li & 7;
+  C.abase = (C.wm * 128 + C.li) * 128 + ((C.lq ^ sw) * 16);
+  C.bbase = A_BYTES + (C.wn * 128 + C.li) * 128 + ((C.lq ^ sw) * 16);
+  C.kh1 = (((4 + C.lq) ^ sw) - (C.lq ^ sw)) * 16;
+  constexpr int BL = BIAS ? 1 : 0;
+  auto panel = [&](int tile) {   // this wave's operand panel of `tile`
+    int tm0, tn0;
+    tile_of(tile, ntn, tm0, tn0);
+    return uniform_rsrc(isb ? (const void*)(g.b + (size_t)tn0 * g.ldb) : (const void*)(g.a + (size_t)tm0 * g.lda));
+  };
+  const auto rbias = uniform_rsrc(BIAS ? (const void*)g.bias : (const void*)g.a);
+  // K-steps 0 and 1 (both of the first tile: nk >= 2)
+  auto rs_cur = panel(t);
+  w4_stage(C, rs_cur, ld, smem, 0, 0, 16);
+  w4_stage(C, rs_cur, ld, smem + TILE_BYTES, 1, 0, 16);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  bar();
+  bf16x8 xa[8], xb[8], ya[8], yb[8];
+  w4_read(smem, C, 0, xa, xb);
+  f32x4 acc[8][8];
+  int m0, n0;
+  tile_of(t, ntn, m0, n0);
+  int it = 0;       // tile iteration of this workgroup
+  int kk = 0;       // K-step within the tile
+  auto rs_next = panel(t + per < end ? t + per : t);
+  (void)kk;
+  for (int gs0 = 0; gs0 < ng; gs0 += nk) {   // one tile
+    for (int k = 0; k < nk; ++k) {
+      const int gs = gs0 + k;
+      const char* cur = smem + (gs & 1) * TILE_BYTES;
+      char* oth = smem + ((gs & 1) ^ 1) * TILE_BYTES;
+      // ---- part 1: k-half 0 MFMAs (X) | k-half 1 reads (Y)
+      w4_read(cur, C, 1, ya, yb);
+      if (k == 0) w4_mfma<true>(acc, xa, xb);
+      else w4_mfma<false>(acc, xa, xb);
+      DTD_W4_SCHED(16, 1, 0, 4);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the DMA of K-step gs + 1 (issued in part 2 of gs - 1 or the prologue); younger: the
+      // epilogue stores of the tile that ended at gs - 1
+      if (k == 0 && it > 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W4_STORES) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      // ---- part 2: k-half 1 MFMAs (Y) | k-half 0 reads of K-step gs + 1 (X) | DMA of K-step gs + 2
+      const bool has1 = gs + 1 < ng, has2 = gs + 2 < ng;
+      if (has1) w4_read(oth, C, 0, xa, xb);
+      if constexpr (BIAS) {
+        if (k == 0)   // this tile's bias -> its LDS slot (waves 0-1: 256 B each)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias,
+                                                    (lds_void*)(smem + LDS_BYTES + (it & 1) * 512 + (w & 1) * 256), 4,
+                                                    (n0 + (w & 1) * 128) * 2 + lane * 4, 0, 0, 0);
+      }
+      if (has2) {
+        // K-step gs + 2: this tile's k + 2, or the next tile's k + 2 - nk
+        const bool nxt = k + 2 >= nk;
+        const auto rs2 = nxt ? rs_next : rs_cur;
+        w4_stage(C, rs2, ld, const_cast<char*>(cur), nxt ? k + 2 - nk : k + 2, 0, 16);
+      }
+      w4_mfma<false>(acc, ya, yb);
+      DTD_W4_SCHED(16, 1, 1, 4);
+    }
+    // ---- tile done: epilogue, then the next tile
+    w4_epilogue<BIAS>(acc, smem + LDS_BYTES + (it & 1) * 512, g.c, g.ldc, m0, n0, C);
+    ++it;
+    t += per;
+    tile_of(t < end ? t : beg, ntn, m0, n0);
+    rs_cur = rs_next;
+    rs_next = panel(t + per < end ? t + per : t);
+  }
+}
+

@@ -3,5 +3,5 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 source scripts/gpu_step.sh
 export TMPDIR=/tmp
-step gemm_v2 300 python scripts/bench_gemm_v2.py
+step gemm_v2 300 env VNEW=5 python scripts/bench_gemm_v2.py
 echo done
