@@ -25,8 +25,11 @@ def main(path):
     steps = []
     for a0, a1 in zip(adam, adam[1:]):
         win = [k for k in ks if a0 <= k[0] < a1]
-        ref = [k for k in win if is_refresh(k[2])]
-        comp = [k for k in win if not is_refresh(k[2])]
+        # the refresh precedes the backward; the backward's reduce-scatters (copies at world 1)
+        # start after its first kernel (the loss / LayerNorm backward)
+        bwd0 = min((k[0] for k in win if "xent_bwd" in k[2] or "ln_bwd" in k[2]), default=a1)
+        ref = [k for k in win if is_refresh(k[2]) and k[0] < bwd0]
+        comp = [k for k in win if not is_refresh(k[2]) and k[0] < bwd0]
         if not ref:
             continue
         tot = sum(e - s for s, e, _, _ in ref)
