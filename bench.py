@@ -110,7 +110,9 @@ def main():
         # zero_dp_training.py's DeepSpeed config (Adam lr 1.5e-4), larger reduce buckets
         zcfg = {"train_micro_batch_size_per_gpu": args.batch_size,
                 "optimizer": {"type": "Adam", "params": {"lr": 1.5e-4}},
-                "zero_optimization": {"stage": args.zero_stage, "reduce_bucket_size": args.reduce_bucket},
+                # the partitioned data flow even at world 1 (the path every rank runs at N > 1)
+                "zero_optimization": {"stage": args.zero_stage, "reduce_bucket_size": args.reduce_bucket,
+                                      "world1_replicated": False},
                 "bf16": {"enabled": dtype == torch.bfloat16}}
         engine, _, _, _ = initialize(model=model, model_parameters=model.parameters(), config=zcfg)
         gdt = engine.grad_dtype

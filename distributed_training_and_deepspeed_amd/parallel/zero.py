@@ -59,7 +59,7 @@ DEFAULTS = {
     "comms_logger": {"enabled": False},
     "zero_optimization": {"stage": 0, "reduce_bucket_size": 5e8, "allgather_bucket_size": 5e8,
                           "overlap_comm": None, "stage3_prefetch_bucket_size": 5e7,
-                          "overlap_param_refresh": True},
+                          "overlap_param_refresh": True, "world1_replicated": True},
 }
 
 
@@ -85,6 +85,7 @@ class ZeroConfig:
         self.allgather_bucket = max(1, int(float(z.get("allgather_bucket_size", 5e8))))
         self.prefetch_bucket = max(0, int(float(z.get("stage3_prefetch_bucket_size", 5e7))))
         self.overlap_refresh = bool(z.get("overlap_param_refresh", True))
+        self.world1_replicated = bool(z.get("world1_replicated", True))
         oc = z.get("overlap_comm")
         self.overlap = (self.stage >= 2) if oc is None else bool(oc)
         bf = cfg.get("bf16", {})
@@ -249,6 +250,17 @@ class ZeroEngine(nn.Module):
             self.gather_group = dist.new_group(ranks=ranks)
         self.shard_world = 1 if self.stage == 0 else self.world
         self.shard_rank = 0 if self.stage == 0 else self.rank
+        # replicated layout (stage 0's): the stage-0 engine, and stages 1/2 on ONE rank, where the
+        # partition is the whole buffer -- reduce-scatter and all-gather are identities, so the
+        # gradient / parameter "shards" alias the flat buffers instead of being copied each step.
+        # `zero_optimization.world1_replicated: false` keeps the partitioned code path at world 1
+        # (bench.py does, so the 1-GPU bench runs the N > 1 data flow).
+        self.replicated = self.stage == 0 or (self.world == 1 and self.stage in (1, 2)
+                                              and self.config.world1_replicated)
+        # stage 3 on one rank: a unit's "gathered" parameters and its gradient landing region are
+        # views of its (whole) shard, so nothing is copied per use (one micro-batch per step)
+        self.alias_units = (self.stage == 3 and self.world == 1 and self.config.world1_replicated
+                            and self.config.gas == 1)
         self.micro_step = 0
         self.global_steps = 0
         self._callback_queued = False
@@ -417,7 +429,7 @@ class ZeroEngine(nn.Module):
                 p.data = v
             off += s.numel
         self.grad_flat = None
-        if self.stage <= 1:
+        if self.stage <= 1 or self.replicated:
             self.grad_flat = torch.zeros(total, dtype=self.grad_dtype, device=dev)
             off = 0
             for s in self.buckets:
@@ -426,7 +438,7 @@ class ZeroEngine(nn.Module):
                     p.main_grad = s.view(s.gbuf, i)
                 off += s.numel
         # ring arenas: gradient landing regions (stages 2/3) and gathered units (stage 3)
-        reg = [s.numel for s in self.segments if self.stage >= 2 or s.unit]
+        reg = [s.numel for s in self.segments if (self.stage >= 2 and not self.replicated) or s.unit]
         big_unit = max([s.numel for s in self.units], default=0)
         self.landing = _Arena(max(4 * max(self.config.reduce_bucket, ALIGN), 3 * big_unit) if reg else 0,
                               self.grad_dtype, dev)
@@ -448,7 +460,7 @@ class ZeroEngine(nn.Module):
                 self.lowp[s.shard_off:s.shard_off + s.chunk].copy_(full[lo:lo + s.chunk])
             for p in s.params:
                 p.data = torch.empty(0, dtype=self.dtype, device=self.device)
-        if self.stage == 0:
+        if self.replicated:
             # replicated optimizer: the shard IS the whole flat buffer -- alias instead of copying
             self.gshard = self.grad_flat
             if self.lowp is not None:
@@ -491,7 +503,7 @@ class ZeroEngine(nn.Module):
                 p._dtd_expect = self._expect
                 p._dtd_touched = False
                 p._dtd_pending = 0
-                if self.stage >= 2 or s.unit:
+                if (self.stage >= 2 and not self.replicated) or s.unit:
                     p._dtd_pre_write_hook = self._pre_write
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._from_autograd))
 
@@ -516,6 +528,12 @@ class ZeroEngine(nn.Module):
             self._alloc_landing(s)
 
     def _alloc_landing(self, s: _Segment) -> None:
+        if s.unit and self.alias_units:   # the unit's gradient shard itself (padding stays zero)
+            s.gbuf = self.gshard[s.shard_off:s.shard_off + s.numel]
+            for i, p in enumerate(s.params):
+                p.main_grad = s.view(s.gbuf, i)
+                p._dtd_touched = False
+            return
         cur = torch.cuda.current_stream(self.device) if self.cuda else None
         s.gbuf = self.landing.acquire(s.numel, s.index, waiter=cur.wait_event if cur is not None else None)
         # padding (alignment gaps, segment tail) must reduce as zeros: the region is recycled
@@ -531,7 +549,8 @@ class ZeroEngine(nn.Module):
         if not self._callback_queued:
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
-        allow = self.config.overlap and not (self.stage <= 1 and not self.is_gradient_accumulation_boundary())
+        full = self.stage <= 1 or self.replicated   # one full gradient buffer, reduced once per step
+        allow = self.config.overlap and not (full and not self.is_gradient_accumulation_boundary())
         _, launch = self.tracker.contribute(self._pindex[id(p)], autograd, allow_launch=allow)
         for k in launch:
             s = self.segments[k]
@@ -559,10 +578,10 @@ class ZeroEngine(nn.Module):
         buf = s.gbuf
         # stages 0/1 accumulate micro-batches in the full gradient buffer and reduce once;
         # stages 2/3 reduce every micro-batch and accumulate the shards
-        first = self.micro_step == 0 or self.stage <= 1
+        first = self.micro_step == 0 or self.stage <= 1 or self.replicated
         out = self.gshard[s.shard_off:s.shard_off + s.chunk]
         with self._comm_ctx():
-            if self.stage == 0:  # buf aliases the gradient "shard" (the full buffer)
+            if self.replicated:  # buf aliases the gradient "shard" (the full buffer)
                 if self.world > 1:
                     op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
                     w = clog.all_reduce(buf, op=op, group=self.group, async_op=True)
@@ -577,16 +596,18 @@ class ZeroEngine(nn.Module):
                     w.wait()
                     if self.backend != "nccl":
                         dst.div_(self.world)
-                else:
+                elif dst.data_ptr() != buf.data_ptr():   # aliased stage-3 unit: already in place
                     dst.copy_(buf)
                 if not first:
                     out.add_(dst)
             ev = None
-            if self.comm_stream is not None and (self.stage >= 2 or s.unit):
+            landed = (self.stage >= 2 and not self.replicated) or s.unit
+            if self.comm_stream is not None and landed:
                 ev = torch.cuda.Event()
                 ev.record(self.comm_stream)
-        if self.stage >= 2 or s.unit:
-            self.landing.release(buf, ev, self.comm_stream)
+        if landed:
+            if not (s.unit and self.alias_units):
+                self.landing.release(buf, ev, self.comm_stream)
             s.gbuf = None
             for p in s.params:
                 p.main_grad = None
@@ -598,7 +619,7 @@ class ZeroEngine(nn.Module):
 
     def _end_of_backward(self) -> None:
         self._callback_queued = False
-        if self.stage <= 1 and not self.is_gradient_accumulation_boundary():
+        if (self.stage <= 1 or self.replicated) and not self.is_gradient_accumulation_boundary():
             return
         for s in self.buckets:
             if not s.launched:
@@ -618,6 +639,11 @@ class ZeroEngine(nn.Module):
 
     def _gather(self, s: _Segment) -> None:
         if s.full is not None:
+            return
+        if self.alias_units:   # one rank: the shard is the whole unit
+            s.full = self.lowp_view[s.shard_off:s.shard_off + s.numel]
+            for i, p in enumerate(s.params):
+                p.data = s.view(s.full, i)
             return
         full = self.gather_arena.acquire(s.numel, s.index)
         src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
@@ -647,8 +673,9 @@ class ZeroEngine(nn.Module):
         if s.gather_event is not None:   # gathered (prefetched) but never used: still order it
             torch.cuda.current_stream(self.device).wait_event(s.gather_event)
             s.gather_event = None
-        self.gather_arena.release(s.full, None,
-                                  torch.cuda.current_stream(self.device) if self.cuda else None)
+        if not self.alias_units:
+            self.gather_arena.release(s.full, None,
+                                      torch.cuda.current_stream(self.device) if self.cuda else None)
         self._set_released(s)
 
     def _prefetch(self, order) -> None:
@@ -708,7 +735,7 @@ class ZeroEngine(nn.Module):
 
     # ================================================================== engine API
     def _reset(self) -> None:
-        accumulate_full = self.stage <= 1 and self.micro_step > 0  # keep accumulating in place
+        accumulate_full = (self.stage <= 1 or self.replicated) and self.micro_step > 0  # keep accumulating in place
         self.tracker.reset()
         self.landing.new_window()
         self.gather_arena.new_window()
@@ -766,7 +793,7 @@ class ZeroEngine(nn.Module):
         refresh each group records an event and the next forward's unit pre-hooks wait for their
         own buckets only; otherwise the compute stream waits for everything here.  Stage 3 units
         stay sharded until their next use."""
-        if self.stage == 0:
+        if self.replicated:
             for s in self.buckets:
                 src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
                 if src.data_ptr() != s.full.data_ptr():   # aliased (the usual case): nothing to copy
@@ -914,7 +941,7 @@ class ZeroEngine(nn.Module):
                 p.data.copy_(sd[names[id(p)][0]])
             lo = self.shard_rank * s.chunk
             self.master[s.shard_off:s.shard_off + s.chunk].copy_(s.full[lo:lo + s.chunk])
-            if self.lowp is not None and self.stage > 0:
+            if self.lowp is not None and not self.replicated:
                 self.lowp[s.shard_off:s.shard_off + s.chunk].copy_(s.full[lo:lo + s.chunk])
         for s in self.units:
             full = torch.zeros(s.numel, dtype=self.dtype, device=self.device)

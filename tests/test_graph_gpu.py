@@ -46,8 +46,8 @@ def test_captured_step_matches_eager():
         assert torch.equal(p, q), n
 
 
-@pytest.mark.parametrize("stage", [0, 1, 2, 3])
-def test_captured_zero_step_matches_eager(stage):
+@pytest.mark.parametrize("stage,replicated", [(0, True), (1, True), (2, True), (3, True), (1, False), (2, False), (3, False)])
+def test_captured_zero_step_matches_eager(stage, replicated):
     """zero_dp_training.py --graph: a replayed ZeRO step (causal LM, fused Adam with device-side
     step count, parameter refresh, RNG advance; stage 2/3 landing regions and stage-3 gathered
     units from the persistent arenas) equals the eager engine step."""
@@ -55,13 +55,14 @@ def test_captured_zero_step_matches_eager(stage):
     from distributed_training_and_deepspeed_amd import comm
     from distributed_training_and_deepspeed_amd.parallel.zero import initialize
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(31000 + os.getpid() % 1000 + stage)
+    os.environ["MASTER_PORT"] = str(31000 + os.getpid() % 1000 + stage + 10 * replicated)
     comm.init(rank=0, world_size=1, backend="nccl", local_rank=0)
     try:
         def setup():
             model = build_model("causal-tiny", dtype=torch.bfloat16, device="cuda", seed=3)
             cfg = {"optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "comms_logger": {"enabled": False},
-                   "zero_optimization": {"stage": stage, "reduce_bucket_size": 100000}}
+                   "zero_optimization": {"stage": stage, "reduce_bucket_size": 100000,
+                                         "world1_replicated": replicated}}
             eng, _, _, _ = initialize(model=model, model_parameters=model.parameters(), config=cfg)
 
             def step(input_ids, labels):

@@ -22,11 +22,11 @@ def rccl_world1():
     comm.destroy()
 
 
-def _zero_run(stage, steps=4):
+def _zero_run(stage, steps=4, replicated=True):
     from distributed_training_and_deepspeed_amd.parallel.zero import initialize
     model = build_model("causal-tiny", dtype=torch.bfloat16, device="cuda", seed=3)
     cfg = {"optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "comms_logger": {"enabled": True},
-           "zero_optimization": {"stage": stage, "reduce_bucket_size": 100000}}
+           "zero_optimization": {"stage": stage, "reduce_bucket_size": 100000, "world1_replicated": replicated}}
     eng, opt, _, _ = initialize(model=model, model_parameters=model.parameters(), config=cfg)
     ds = SyntheticLMDataset(model.cfg, 4 * steps, seq_len=128, mlm=False, seed=1)
     ids, lab = ds.input_ids.view(steps, 4, 128).cuda(), ds.labels.view(steps, 4, 128).cuda()
@@ -40,10 +40,14 @@ def _zero_run(stage, steps=4):
     return losses, eng.master.detach().float().clone(), eng
 
 
-@pytest.mark.parametrize("stage", [1, 2, 3])
-def test_zero_stages_on_gpu_match_stage0(rccl_world1, stage):
+@pytest.mark.parametrize("stage,replicated", [(1, False), (2, False), (3, False), (1, True), (2, True), (3, True)])
+def test_zero_stages_on_gpu_match_stage0(rccl_world1, stage, replicated):
+    """Stages 1-3 train like stage 0 on one GPU, through the partitioned data flow (landing
+    arena, reduce-scatter / refresh stand-ins, overlapped refresh) and through the world-1
+    replicated layout (stages 1/2 alias the flat buffers)."""
     l0, m0, _ = _zero_run(0)
-    ls, ms, eng = _zero_run(stage)
+    ls, ms, eng = _zero_run(stage, replicated=replicated)
+    assert eng.replicated == (replicated and stage <= 2) and eng.alias_units == (replicated and stage == 3)
     assert all(torch.isfinite(torch.tensor(ls)))
     assert abs(l0[-1] - ls[-1]) < 5e-3, (l0, ls)
     # world 1: every layout holds the same parameter set (different order for stage 3 units)
