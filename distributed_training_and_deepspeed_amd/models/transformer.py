@@ -201,6 +201,11 @@ class TransformerLayer(nn.Module):
 
 # qkv bias gradient from the attention-backward epilogues (DTD_ATTN_QKV_BIAS=0: separate pass)
 _FUSED_QKV_BIAS = [os.environ.get("DTD_ATTN_QKV_BIAS", "1") == "1"]
+# Memory-efficient post-LN LayerNorms (DTD_LN_MEMEFF=0: store z): the forward keeps no
+# z = residual + dropout(y) -- the backward recomputes x-hat = (out - beta) / gamma from the LN
+# output, which the layer keeps anyway (fc1's input / the next layer's input).  One [T, h] write
+# per LayerNorm forward and one [T, h] activation per LayerNorm less.
+_LN_MEMEFF = [os.environ.get("DTD_LN_MEMEFF", "1") == "1"]
 
 
 def _acc(p):
@@ -245,10 +250,11 @@ class _FusedLayerFn(torch.autograd.Function):
         qkv = F.linear(a_in, qkv_w, qkv_b)
         actx, lse, amask = A.attn_fwd(qkv, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, masks=pend)
         o = F.linear(actx, o_w, o_b)
+        ln_fo = _LN_MEMEFF[0] and not c.pre_ln
         if c.pre_ln:
             z1, f_in, m2, r2 = Fx.ln_fwd(o, x2d, g2, b2, eps, p_h, rng, s1)
         else:
-            z1, f_in, m1, r1 = Fx.ln_fwd(o, x2d, g1, b1, eps, p_h, rng, s1)
+            z1, f_in, m1, r1 = Fx.ln_fwd(o, x2d, g1, b1, eps, p_h, rng, s1, store_z=not ln_fo)
         ffn_g = False   # u holds act'(pre-activation) instead of the pre-activation
         if G.ffn_fwd_enabled() and _ffn_gemm_ok(c, f_in, w1):
             if rt.keep_ffn_act and c.activation in G.GRAD_ACTS and G.ffn_store_grad_enabled():
@@ -266,12 +272,14 @@ class _FusedLayerFn(torch.autograd.Function):
             out = Fx.dropout_add(y, z1, p_h, rng, s2)
             z2 = m3 = r3 = None
         else:
-            z2, out, m3, r3 = Fx.ln_fwd(y, f_in, g2, b2, eps, p_h, rng, s2)
+            z2, out, m3, r3 = Fx.ln_fwd(y, f_in, g2, b2, eps, p_h, rng, s2, store_z=not ln_fo)
         a_keep = a if rt.keep_ffn_act else None
         if c.pre_ln:
             ctx.save_for_backward(x2d, a_in, qkv, actx, lse, z1, f_in, u, m1, r1, m2, r2, a_keep)
         else:
-            ctx.save_for_backward(x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3, a_keep)
+            # memory-efficient form: the LN2 output stands in for z2 (z1's stand-in, f_in, is saved)
+            ctx.save_for_backward(x2d, qkv, actx, lse, z1, f_in, u, m1, r1, out if ln_fo else z2, m3, r3, a_keep)
+        ctx.ln_fo = ln_fo
         ctx.layer = layer
         ctx.amask = amask  # attention dropout keep bits (kernel path) for the backward
         ctx.rng = rng  # the RngState of this forward's device (pipeline stages differ)
@@ -296,8 +304,9 @@ class _FusedLayerFn(torch.autograd.Function):
         else:
             x2d, qkv, actx, lse, z1, f_in, u, m1, r1, z2, m3, r3, a = ctx.saved_tensors
             # out = LN2(f_in + dropout(y)); dz2 = d(out)/d(z2), flows to f_in (residual) and y
-            dz2, dy = Fx.ln_bwd(dout, None, z2, m3, r3, g2, p_h, rng, s2, want_dz=True, want_dy=True,
-                                dgamma=_acc(g2), dbeta=_acc(b2), dbias=_acc(bf2))
+            lo2 = dict(xout=z2, beta=b2) if ctx.ln_fo else {}
+            dz2, dy = Fx.ln_bwd(dout, None, None if ctx.ln_fo else z2, m3, r3, g2, p_h, rng, s2, want_dz=True,
+                                want_dy=True, dgamma=_acc(g2), dbeta=_acc(b2), dbias=_acc(bf2), **lo2)
             for p in (g2, b2, bf2):
                 grad_done(p)
         # dgrad first; without a kept forward activation, a = act(u) (fc2's wgrad input) is
@@ -339,8 +348,9 @@ class _FusedLayerFn(torch.autograd.Function):
             # f_in = LN1(z1) feeds both the FFN and (as residual) z2: d f_in = du.W1 + dz2, with
             # the residual term summed inside the LN kernel (no addmm C-copy, no add pass)
             dfin = du @ w1
+            lo1 = dict(xout=f_in, beta=b1) if ctx.ln_fo else {}
             dz1, do = Fx.ln_bwd(dfin, None, z1, m1, r1, g1, p_h, rng, s1, want_dz=True, want_dy=True,
-                                dgamma=_acc(g1), dbeta=_acc(b1), dbias=_acc(o_b), dout2=dz2)
+                                dgamma=_acc(g1), dbeta=_acc(b1), dbias=_acc(o_b), dout2=dz2, **lo1)
             for p in (g1, b1, o_b):
                 grad_done(p)
         emit_wgrad(o_w, do, actx, async_ok=True)

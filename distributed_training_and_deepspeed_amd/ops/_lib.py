@@ -33,6 +33,7 @@ _SIGS = {
     "dtd_ln_bwd_num_partials": (I, [I, I]),
     "dtd_ln_fwd": (I, [I, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, P]),
     "dtd_ln_bwd": (I, [I, P, P, P, P, P, P, P, P, P, P, P, P, I, I, F, P, U32, P]),
+    "dtd_ln_bwd_fo": (I, [I, P, P, P, P, P, P, P, P, P, P, P, P, I, I, F, P, U32, P]),
     # act.hip
     "dtd_act_fwd": (I, [I, P, P, SZ, I, P]),
     "dtd_act_bwd_num_partials": (I, [I, I]),

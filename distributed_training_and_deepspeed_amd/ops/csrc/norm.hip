@@ -33,6 +33,7 @@ struct LnBwdArgs {
   const void* dz_extra; const void* z; const float* mean; const float* rstd;
   const void* gamma; void* dz; void* dy; float* part_gamma; float* part_beta; float* part_bias;
   int rows, h; float p; const uint64_t* rng; uint32_t stream_id;
+  const void* xo; const void* beta;     // memory-efficient form: LN output + beta instead of z / mean
 };
 
 // keep/scale for element e of a [rows, h] tensor.
@@ -116,45 +117,106 @@ __global__ void __launch_bounds__(256) ln_fwd_wave(LnFwdArgs a) {
   }
 }
 
+// Raw (unconverted) VEC-element vector of a [rows, h] tensor: the backward's next-row prefetch
+// holds its loads packed (bf16: VEC / 2 registers) until the row is processed.
+template <typename T, int N> struct RawVec { typedef T type __attribute__((ext_vector_type(N))); };
+template <typename T, int VEC, int NT>
+__device__ __forceinline__ typename RawVec<T, VEC>::type ld_raw(const T* p) {
+  typedef typename RawVec<T, VEC>::type vt;
+  if constexpr ((NT & 1) != 0) return __builtin_nontemporal_load(reinterpret_cast<const vt*>(p));
+  else return *reinterpret_cast<const vt*>(p);
+}
+
+// x-hat of the memory-efficient backward (FO): the forward stored only its output
+// o = x-hat * gamma + beta, so x-hat = (o - beta) / gamma (reciprocal of gamma held per lane;
+// |gamma| is clamped at 1e-12 -- an exactly-zero gamma column gets x-hat 0 and no dgamma, the
+// known limit of the form).
+__device__ __forceinline__ float safe_rcp(float g) {
+  return 1.f / (fabsf(g) < 1e-12f ? copysignf(1e-12f, g) : g);
+}
+
 // One row per wave (the two-rows-per-wave layout of the forward doubles this kernel's per-lane
-// state and costs occupancy).
-template <typename T, int VEC, int ITERS, int NT>
+// state and costs occupancy).  The row loop is software-pipelined: the next row's loads (z or the
+// LN output, dout, dout2, rstd) are issued before this row's reductions, so each wave keeps one
+// row of HBM reads in flight behind its arithmetic instead of a serial load -> reduce -> store
+// chain.  FO: x-hat from the LN output (LnBwdArgs::xo, beta) instead of z and the mean.
+template <typename T, int VEC, int ITERS, int NT, bool FO, bool PF>
 __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
   constexpr int NPL = VEC * ITERS, LPR = 64;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6, sub = lane;
+  typedef typename RawVec<T, VEC>::type vt;
+  // the row is wave-uniform: readfirstlane lets hipcc keep the row base in SGPRs (saddr loads /
+  // stores with a 32-bit lane offset) instead of a 64-bit address pair per access
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
+  const int sub = lane;
   const int h = a.h;
   const bool has_drop = a.p > 0.f && a.dy != nullptr;
   DropoutRng g(a.rng, a.stream_id);
   const uint32_t thr = keep_threshold(a.p);
   const float scale = has_drop ? 1.f / (1.f - a.p) : 1.f;
-  float pg[NPL], pb[NPL], py[NPL], gm[NPL];
+  float pg[NPL], pb[NPL], py[NPL];
+  // gamma / beta stay packed (bf16: VEC / 2 registers per chunk) and are widened at each use.
+  // FO: they are re-read (L1 / L2 hits) with each row's loads -- the compiler barrier in front
+  // stops hipcc from hoisting 2 x NPL widened loop invariants into registers (4 -> 3 waves / SIMD)
+  vt gmr[ITERS], btr[FO ? ITERS : 1];
 #pragma unroll
   for (int i = 0; i < NPL; ++i) { pg[i] = 0.f; pb[i] = 0.f; py[i] = 0.f; }
+  if constexpr (!FO) {
 #pragma unroll
-  for (int c = 0; c < ITERS; ++c) vload<T, VEC>((const T*)a.gamma + (c * LPR + sub) * VEC, gm + c * VEC);
-
-  for (int row = blockIdx.x * nw + w; row < a.rows; row += gridDim.x * nw) {
+    for (int c = 0; c < ITERS; ++c) gmr[c] = ld_raw<T, VEC, 0>((const T*)a.gamma + (c * LPR + sub) * VEC);
+  }
+  const T* src = (const T*)(FO ? a.xo : a.z);
+  const bool two = a.dout2 != nullptr;
+  const int stride = gridDim.x * nw;
+  vt nz[ITERS], nd[ITERS], ne[ITERS];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int r) {
+    const size_t b = (size_t)r * h;
+    if constexpr (FO) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int c = 0; c < ITERS; ++c) {
+        gmr[c] = ld_raw<T, VEC, 0>((const T*)a.gamma + (c * LPR + sub) * VEC);
+        btr[c] = ld_raw<T, VEC, 0>((const T*)a.beta + (c * LPR + sub) * VEC);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < ITERS; ++c) {
+      const int col = (c * LPR + sub) * VEC;
+      nz[c] = ld_raw<T, VEC, NT>(src + b + col);
+      nd[c] = ld_raw<T, VEC, NT>((const T*)a.dout + b + col);
+      if (two) ne[c] = ld_raw<T, VEC, NT>((const T*)a.dout2 + b + col);
+    }
+    if constexpr (!FO) nmu = a.mean[r];
+    nrs = a.rstd[r];
+  };
+  int row = blockIdx.x * nw + w;
+  if (PF && row < a.rows) fetch(row);
+  for (; row < a.rows; row += stride) {
     const size_t base = (size_t)row * h;
-    const float mu = a.mean[row], rs = a.rstd[row];
+    if (!PF) fetch(row);
+    vt cz[ITERS], cd[ITERS], ce[ITERS];
+#pragma unroll
+    for (int c = 0; c < ITERS; ++c) { cz[c] = nz[c]; cd[c] = nd[c]; ce[c] = ne[c]; }
+    const float mu = nmu, rs = nrs;
+    if (PF && row + stride < a.rows) fetch(row + stride);
     float xh[NPL], dg[NPL];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < ITERS; ++c) {
-      const int col = (c * LPR + sub) * VEC;
       float zz[VEC], dd[VEC];
-      LDNT((const T*)a.z + base + col, zz);
-      LDNT((const T*)a.dout + base + col, dd);
-      if (a.dout2) {
-        float e[VEC];
-        LDNT((const T*)a.dout2 + base + col, e);
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) dd[j] += e[j];
+      for (int j = 0; j < VEC; ++j) {
+        zz[j] = (float)cz[c][j];
+        dd[j] = (float)cd[c][j];
+        if (two) dd[j] += (float)ce[c][j];
       }
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         const int i = c * VEC + j;
-        xh[i] = (zz[j] - mu) * rs;
-        dg[i] = dd[j] * gm[i];
+        const float gmv = (float)gmr[c][j];
+        if constexpr (FO) xh[i] = (zz[j] - (float)btr[c][j]) * safe_rcp(gmv);
+        else xh[i] = (zz[j] - mu) * rs;
+        dg[i] = dd[j] * gmv;
         s1 += dg[i];
         s2 += dg[i] * xh[i];
         pg[i] += dd[j] * xh[i];
@@ -285,17 +347,32 @@ __global__ void __launch_bounds__(256) ln_bwd_block(LnBwdArgs a) {
   __syncthreads();
   for (int row = blockIdx.x; row < a.rows; row += gridDim.x) {
     const size_t base = (size_t)row * h;
-    const float mu = a.mean[row], rs = a.rstd[row];
+    const float mu = a.xo ? 0.f : a.mean[row], rs = a.rstd[row];
+    // x-hat of column pair col: from z and the mean, or (memory-efficient form) from the output
+    auto xhat = [&](int col, const float* gm, float* xh) {
+      float zz[2];
+      if (a.xo) {
+        float bt[2];
+        vload<T, 2>((const T*)a.xo + base + col, zz);
+        vload<T, 2>((const T*)a.beta + col, bt);
+        xh[0] = (zz[0] - bt[0]) * safe_rcp(gm[0]);
+        xh[1] = (zz[1] - bt[1]) * safe_rcp(gm[1]);
+      } else {
+        vload<T, 2>((const T*)a.z + base + col, zz);
+        xh[0] = (zz[0] - mu) * rs;
+        xh[1] = (zz[1] - mu) * rs;
+      }
+    };
     float s1 = 0.f, s2 = 0.f;
     for (int col = threadIdx.x * 2; col < h; col += blockDim.x * 2) {
-      float zz[2], dd[2], gm[2];
-      vload<T, 2>((const T*)a.z + base + col, zz);
+      float xv[2], dd[2], gm[2];
       vload<T, 2>((const T*)a.dout + base + col, dd);
       if (a.dout2) { float e[2]; vload<T, 2>((const T*)a.dout2 + base + col, e); dd[0] += e[0]; dd[1] += e[1]; }
       vload<T, 2>((const T*)a.gamma + col, gm);
+      xhat(col, gm, xv);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float xh = (zz[j] - mu) * rs, dg = dd[j] * gm[j];
+        const float xh = xv[j], dg = dd[j] * gm[j];
         s1 += dg; s2 += dg * xh;
         if (pgp) pgp[col + j] += dd[j] * xh;   // same thread owns the same columns every row
         if (pbp) pbp[col + j] += dd[j];
@@ -303,14 +380,14 @@ __global__ void __launch_bounds__(256) ln_bwd_block(LnBwdArgs a) {
     }
     const float m1 = block_sum(s1, red) / h, m2 = block_sum(s2, red) / h;
     for (int col = threadIdx.x * 2; col < h; col += blockDim.x * 2) {
-      float zz[2], dd[2], gm[2], dz[2];
-      vload<T, 2>((const T*)a.z + base + col, zz);
+      float xv[2], dd[2], gm[2], dz[2];
       vload<T, 2>((const T*)a.dout + base + col, dd);
       if (a.dout2) { float e[2]; vload<T, 2>((const T*)a.dout2 + base + col, e); dd[0] += e[0]; dd[1] += e[1]; }
       vload<T, 2>((const T*)a.gamma + col, gm);
+      xhat(col, gm, xv);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float xh = (zz[j] - mu) * rs, dg = dd[j] * gm[j];
+        const float xh = xv[j], dg = dd[j] * gm[j];
         dz[j] = rs * (dg - m1 - xh * m2);
       }
       if (a.dz_extra) { float e[2]; vload<T, 2>((const T*)a.dz_extra + base + col, e); dz[0] += e[0]; dz[1] += e[1]; }
@@ -328,6 +405,25 @@ __global__ void __launch_bounds__(256) ln_bwd_block(LnBwdArgs a) {
   }
 }
 
+// DTD_LN_BWD_PREFETCH=1: the software-pipelined row loop (next row's loads in flight behind this
+// row's arithmetic, at 3 waves / SIMD); 0: one row's loads at a time at 4 waves / SIMD.
+inline bool ln_bwd_prefetch() {
+  const char* e = getenv("DTD_LN_BWD_PREFETCH");   // read per call (A/B tests flip it in-process)
+  return e != nullptr && atoi(e) != 0;
+}
+
+template <typename T, int VEC, int ITERS, bool PF>
+void launch_bwd(const LnBwdArgs& b, int nblocks, int nt, hipStream_t s) {
+  const dim3 grid(nblocks), block(256);
+  if (b.xo) {
+    if (nt == 3) hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, 3, true, PF>), grid, block, 0, s, b);
+    else hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, 0, true, PF>), grid, block, 0, s, b);
+  } else {
+    if (nt == 3) hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, 3, false, PF>), grid, block, 0, s, b);
+    else hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, 0, false, PF>), grid, block, 0, s, b);
+  }
+}
+
 template <typename T, int VEC, int ITERS, int LPR = 64>
 bool try_wave(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream_t s) {
   const int h = f ? f->h : b->h;
@@ -340,11 +436,10 @@ bool try_wave(const LnFwdArgs* f, const LnBwdArgs* b, int nblocks_bwd, hipStream
       case 3: hipLaunchKernelGGL((ln_fwd_wave<T, VEC, ITERS, LPR, 3>), grid, dim3(256), 0, s, *f); break;
       default: hipLaunchKernelGGL((ln_fwd_wave<T, VEC, ITERS, LPR, 0>), grid, dim3(256), 0, s, *f); break;
     }
+  } else if (ln_bwd_prefetch()) {
+    launch_bwd<T, VEC, ITERS, true>(*b, nblocks_bwd, nt, s);
   } else {
-    switch (nt) {
-      case 3: hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, 3>), dim3(nblocks_bwd), dim3(256), 0, s, *b); break;
-      default: hipLaunchKernelGGL((ln_bwd_wave<T, VEC, ITERS, 0>), dim3(nblocks_bwd), dim3(256), 0, s, *b); break;
-    }
+    launch_bwd<T, VEC, ITERS, false>(*b, nblocks_bwd, nt, s);
   }
   return true;
 }
@@ -457,8 +552,10 @@ DTD_EXPORT int dtd_ln_bwd_num_partials(int rows, int h) {
   if (wave_shape(h)) {
     // up to 1024 blocks x 4 waves = 4 waves per SIMD on 256 CUs: the row loop is a serial chain
     // of loads -> wave reductions -> stores, so occupancy is what hides HBM latency
+    // (the prefetching form holds 3 waves / SIMD: 768 blocks)
+    const int cap = ln_bwd_prefetch() ? 768 : 1024;
     int blocks = (rows + 3) / 4;
-    return blocks < 1024 ? blocks : 1024;
+    return blocks < cap ? blocks : cap;
   }
   return rows < 256 ? rows : 256;
 }
@@ -479,7 +576,23 @@ DTD_EXPORT int dtd_ln_bwd(int dtype, const void* dout, const void* dout2, const 
                           float p, const uint64_t* rng, uint32_t stream_id, hipStream_t s) {
   if (rows <= 0) return 0;
   LnBwdArgs a{dout, dout2, dz_extra, z, mean, rstd, gamma, dz, dy, part_gamma, part_beta, part_bias,
-              rows, h, p, rng, stream_id};
+              rows, h, p, rng, stream_id, nullptr, nullptr};
+  const int nb = dtd_ln_bwd_num_partials(rows, h);
+  if (dtype == kBF16) dispatch<bf16>(nullptr, &a, nb, s);
+  else dispatch<float>(nullptr, &a, nb, s);
+  DTD_LAUNCH_CHECK();
+}
+
+// Memory-efficient backward: x-hat recomputed from the LayerNorm output xo = x-hat * gamma + beta
+// (the forward stored no z; Apex's memory_efficient LayerNorm form).  Same outputs as dtd_ln_bwd.
+DTD_EXPORT int dtd_ln_bwd_fo(int dtype, const void* dout, const void* dout2, const void* dz_extra, const void* xo,
+                             const void* beta, const float* rstd, const void* gamma, void* dz, void* dy,
+                             float* part_gamma, float* part_beta, float* part_bias, int rows, int h, float p,
+                             const uint64_t* rng, uint32_t stream_id, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (xo == nullptr || beta == nullptr) return (int)hipErrorInvalidValue;
+  LnBwdArgs a{dout, dout2, dz_extra, nullptr, nullptr, rstd, gamma, dz, dy, part_gamma, part_beta, part_bias,
+              rows, h, p, rng, stream_id, xo, beta};
   const int nb = dtd_ln_bwd_num_partials(rows, h);
   if (dtype == kBF16) dispatch<bf16>(nullptr, &a, nb, s);
   else dispatch<float>(nullptr, &a, nb, s);

@@ -135,15 +135,27 @@ def _finalize(part: torch.Tensor, n: int, cols: int, dst, acc: bool, scale: floa
 
 def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: int,
            want_dz: bool = True, want_dy: bool = False,
-           dgamma=None, dbeta=None, dbias=None, acc: bool = False, dout2=None):
+           dgamma=None, dbeta=None, dbias=None, acc: bool = False, dout2=None, xout=None, beta=None):
     """Backward of ``ln_fwd``.  Returns (dz, dy); writes dgamma/dbeta/dbias (bias of the
     producer of y, i.e. column sums of dy) into the destination tensors.  ``dout2``: a second
-    upstream gradient summed into ``dout`` inside the kernel (residual branches)."""
+    upstream gradient summed into ``dout`` inside the kernel (residual branches).
+
+    Memory-efficient form (``z=None``, ``xout``/``beta`` given): x-hat is recomputed from the
+    forward's output, x-hat = (xout - beta) / gamma, so the forward need not store z
+    (``ln_fwd(store_z=False)``); ``mean`` is then unused."""
     rows = dout.numel() // dout.shape[-1]
     h = dout.shape[-1]
+    fo = z is None
+    if fo and (xout is None or beta is None):
+        raise ValueError("ln_bwd: z=None needs the LayerNorm output (xout) and beta")
     if not _on_gpu(dout):
-        zf = z.float().view(rows, h)
-        xh = (zf - mean[:, None]) * rstd[:, None]
+        if fo:
+            g32 = gamma.float()
+            g32 = torch.where(g32.abs() < 1e-12, torch.full_like(g32, 1e-12).copysign(g32), g32)
+            xh = (xout.float().view(rows, h) - beta.float()) / g32
+        else:
+            zf = z.float().view(rows, h)
+            xh = (zf - mean[:, None]) * rstd[:, None]
         d = dout.float().view(rows, h)
         if dout2 is not None:
             d = d + dout2.float().view(rows, h)
@@ -171,10 +183,18 @@ def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: i
     pg = part[next(slots)] if dgamma is not None else None
     pb = part[next(slots)] if dbeta is not None else None
     py = part[next(slots)] if (dbias is not None and want_dy) else None
-    _lib.call("dtd_ln_bwd", _lib.dt(dout), dout.data_ptr(), _lib.ptr(dout2), _lib.ptr(dz_extra), z.data_ptr(),
-              mean.data_ptr(),
-              rstd.data_ptr(), gamma.data_ptr(), _lib.ptr(dz), _lib.ptr(dy), _lib.ptr(pg), _lib.ptr(pb),
-              _lib.ptr(py), rows, h, float(p if want_dy else 0.0), rng.state.data_ptr(), sid, _lib.stream())
+    if fo:
+        xout = xout.contiguous()
+        assert xout.shape == dout.shape and xout.dtype == dout.dtype
+        _lib.call("dtd_ln_bwd_fo", _lib.dt(dout), dout.data_ptr(), _lib.ptr(dout2), _lib.ptr(dz_extra),
+                  xout.data_ptr(), beta.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), _lib.ptr(dz), _lib.ptr(dy),
+                  _lib.ptr(pg), _lib.ptr(pb), _lib.ptr(py), rows, h, float(p if want_dy else 0.0),
+                  rng.state.data_ptr(), sid, _lib.stream())
+    else:
+        _lib.call("dtd_ln_bwd", _lib.dt(dout), dout.data_ptr(), _lib.ptr(dout2), _lib.ptr(dz_extra), z.data_ptr(),
+                  mean.data_ptr(),
+                  rstd.data_ptr(), gamma.data_ptr(), _lib.ptr(dz), _lib.ptr(dy), _lib.ptr(pg), _lib.ptr(pb),
+                  _lib.ptr(py), rows, h, float(p if want_dy else 0.0), rng.state.data_ptr(), sid, _lib.stream())
     dsts = [d for d, on in ((dgamma, pg is not None), (dbeta, pb is not None), (dbias, py is not None)) if on]
     if dsts:
         args = []

@@ -1,0 +1,52 @@
+#!/usr/bin/env python
+"""PMC probe: the persistent NT GEMM (ops/csrc/gemm.hip) vs hipBLASLt on the same products, for
+rocprofv3 --pmc passes (scripts/sessions/gpu_session_r3_gemm_pmc.sh).  Shapes (T = 131072): fc2
+forward (N 768, K 3072: long main loop) and qkv forward (N 2304, K 768: short).  Three launches each;
+`summarize` folds a counter CSV into per-kernel-family means (ours vs hipBLASLt)."""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run():
+    from distributed_training_and_deepspeed_amd.ops import gemm as G
+    from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
+    use_tuned_gemms()
+    T = 131072
+    for N, K in ((768, 3072), (2304, 768)):
+        a = torch.rand(T, K, device="cuda", dtype=torch.bfloat16) * 2 - 1
+        b = torch.rand(N, K, device="cuda", dtype=torch.bfloat16) * 2 - 1
+        c = torch.empty(T, N, device="cuda", dtype=torch.bfloat16)
+        for _ in range(3):
+            G._call(G.EPI_STORE, a, b, c)
+            torch.nn.functional.linear(a, b)
+    torch.cuda.synchronize()
+    print("ok", flush=True)
+
+
+def summarize(paths):
+    acc = defaultdict(lambda: defaultdict(list))
+    for path in paths:
+        for r in csv.DictReader(open(path)):
+            name = r.get("Kernel_Name", "")
+            fam = "ours" if "gemm_bt" in name else ("hipblaslt" if "Cijk" in name else None)
+            if fam is None:
+                continue
+            grid = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
+            key = f"{fam}:{r.get('Kernel_Name')[:60]}:grid{grid}"
+            acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "summarize":
+        summarize(sys.argv[2:])
+    else:
+        run()

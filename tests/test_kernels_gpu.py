@@ -89,6 +89,36 @@ def test_layernorm_fwd_bwd(h, dtype):
         close(a, b, tol)
 
 
+@pytest.mark.parametrize("h", [768, 1024, 2304])
+@pytest.mark.parametrize("prefetch", ["0", "1"])
+def test_layernorm_bwd_from_output(h, prefetch, monkeypatch):
+    """Memory-efficient LN backward (x-hat from the stored output, no z) on the GPU vs the fp32
+    CPU backward from z; both row-loop forms of the wave kernel (h = 2304: block kernel)."""
+    monkeypatch.setenv("DTD_LN_BWD_PREFETCH", prefetch)
+    torch.manual_seed(2)
+    rows, dtype = 4099, torch.bfloat16
+    g, c = rng_pair()
+    y = torch.randn(rows, h, dtype=dtype)
+    r = torch.randn(rows, h, dtype=dtype)
+    gamma = (1 + 0.1 * torch.randn(h)).to(dtype)
+    beta = (0.1 * torch.randn(h)).to(dtype)
+    dout = torch.randn(rows, h, dtype=dtype)
+    dout2 = torch.randn(rows, h, dtype=dtype)
+    outs = {}
+    for dev, rng in ((DEV, g), ("cpu", c)):
+        fo = dev != "cpu"
+        z, o, m, rs = Fx.ln_fwd(y.to(dev), r.to(dev), gamma.to(dev), beta.to(dev), 1e-5, 0.1, rng, 5,
+                                store_z=not fo)
+        assert (z is None) == fo
+        dg, db, dbias = (torch.zeros(h, dtype=torch.float32, device=dev) for _ in range(3))
+        kw = dict(xout=o, beta=beta.to(dev)) if fo else {}
+        dz, dy = Fx.ln_bwd(dout.to(dev), None, z, m, rs, gamma.to(dev), 0.1, rng, 5, want_dz=True, want_dy=True,
+                           dgamma=dg, dbeta=db, dbias=dbias, dout2=dout2.to(dev), **kw)
+        outs[dev] = (o, dz, dy, dg, db, dbias)
+    for a, b in zip(outs[DEV], outs["cpu"]):
+        close(a, b, 3e-2)
+
+
 @pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "relu"])
 def test_activation_fwd_bwd(act):
     torch.manual_seed(1)

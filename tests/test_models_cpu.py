@@ -53,6 +53,15 @@ def test_fused_backward_matches_autograd(name, extra):
         assert err <= 1e-4 * (p1.grad.abs().max().item() + 1e-8), (n, err)
 
 
+@pytest.mark.parametrize("memeff", [True, False])
+def test_post_ln_backward_with_and_without_stored_z(memeff, monkeypatch):
+    """Post-LN (BERT) layers: the memory-efficient LayerNorm backward (x-hat from the LN output,
+    no z kept by the forward; the default) and the stored-z backward both equal autograd."""
+    from distributed_training_and_deepspeed_amd.models import transformer as TR
+    monkeypatch.setattr(TR, "_LN_MEMEFF", [memeff])
+    test_fused_backward_matches_autograd("tiny", {})
+
+
 def test_mlm_masking_law():
     cfg = C.BERT_BASE
     ds = SyntheticLMDataset(cfg, 64, seq_len=512, seed=0)
