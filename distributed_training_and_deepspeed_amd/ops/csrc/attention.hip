@@ -33,6 +33,7 @@
 #include <stdio.h>
 #include <type_traits>
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 
@@ -69,6 +70,34 @@ __device__ __forceinline__ bf16x8 tr_operand(const bf16* tile, int stride, int r
   const int hh = lane >> 5, g = (lane >> 4) & 1, li = lane & 15;
   const bf16* p = tile + (row0 + 4 * hh + (li >> 2)) * stride + col0 + 16 * g + 4 * (li & 3);
   return cat(tr_read(p), tr_read(p + 8 * stride));
+}
+
+// 64-column (D = 64) Q / dO / K tiles of the backward kernels: unpadded 128-byte rows whose
+// 16-byte chunk index is XOR-swizzled by swz64(row) (bits 1, 2 and 1^3 of the row).  Both reads of
+// such a tile are then bank-conflict free: the row-operand ds_read_b128 (16-lane groups of 16 rows
+// at one chunk: distinct (row parity, chunk ^ swz) slots) and the transposed operand read
+// ds_read_b64_tr_b16 (4 rows x 2 column blocks per 32-lane half; rows 4k and 4k+2 land in
+// different 4-chunk groups).  The padded D + 8 pitch left the transposed reads 2-way conflicted
+// (rows r and r + 2 are 72 dwords = 8 banks apart, the second column block's offset) -- 1.6 M
+// (dQ) and 3.2 M (dK/dV) conflict cycles per dispatch (profiles/r2_attention_pmc.json).
+// swz64 depends on row bits 1..3 only, so blocks starting at a multiple of 16 rows share it.
+__device__ __forceinline__ int swz64(int row) {
+  return ((row >> 1) & 1) | (((row >> 2) & 1) << 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 2);
+}
+// element offset of 16-byte chunk `ch` (0..7) of row `row`
+__device__ __forceinline__ int swz64_off(int row, int ch) { return row * 64 + 8 * (ch ^ swz64(row)); }
+// row operand (ds_read_b128) of the swizzled tile: row row0 + r (row0 % 16 == 0), chunk ch
+__device__ __forceinline__ bf16x8 swz_row_read(const bf16* tile, int row0, int r, int ch) {
+  return *reinterpret_cast<const bf16x8*>(tile + row0 * 64 + swz64_off(r, ch));
+}
+// tr_operand on the swizzled tile (row0 % 16 == 0, col0 % 32 == 0)
+__device__ __forceinline__ bf16x8 tr_operand_swz(const bf16* tile, int row0, int col0, int lane) {
+  const int hh = lane >> 5, g = (lane >> 4) & 1, li = lane & 15;
+  const int rl = 4 * hh + (li >> 2);                  // rows rl and rl + 8 of the 16-row block
+  const int ch = (col0 >> 3) + 2 * g + ((li >> 1) & 1);
+  const int e = 4 * (li & 1);
+  const bf16* base = tile + row0 * 64 + e;
+  return cat(tr_read(base + swz64_off(rl, ch)), tr_read(base + swz64_off(rl + 8, ch)));
 }
 
 // Raw v_exp_f32 (2^x): the softmax arguments are <= 0, so the libm wrapper's denormal
@@ -324,6 +353,20 @@ struct TileLoader {
       *reinterpret_cast<bf16x8*>(lds + (c / (D / 8)) * stride + (c % (D / 8)) * 8) = reg[i];
     }
   }
+  // D = 64: the swizzled 128-byte-row image (swz64_off); 8 contiguous lanes fill one row
+  __device__ __forceinline__ void store_swz(bf16* lds) const {
+    static_assert(D == 64, "swizzled tile image is for 64-column tiles");
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      *reinterpret_cast<bf16x8*>(lds + swz64_off(c >> 3, c & 7)) = reg[i];
+    }
+  }
+  // the image the backward kernels use: swizzled for D = 64, padded rows of `stride` otherwise
+  __device__ __forceinline__ void store_bwd(bf16* lds, int stride) const {
+    if constexpr (D == 64) store_swz(lds);
+    else store(lds, stride);
+  }
 };
 
 // grid: (ceil(S/128), B*H); block 256 = 4 waves x 32 queries.  KV tiles of BN keys,
@@ -514,6 +557,185 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   if (hh == 0) a.lse[(size_t)bh * S + q] = (m + log2f(l)) * kLn2;
 }
 
+// Software-pipelined forward (D = 64; DTD_ATTN_FWD=pipe): the score MFMAs of K/V tile t+1 are
+// issued BEFORE tile t's softmax, so within one wave the matrix pipe works on S(t+1) while the
+// VALU runs tile t's max / exp / dropout / row sums (cdna_hip_programming.md T15) -- the serial
+// MFMA -> VALU -> MFMA chain of attn_fwd_kernel leaves the pipe idle unless another wave of the
+// SIMD happens to be in its MFMA phase.  Costs a second 32-register score accumulator.
+// K runs one tile ahead of V through the LDS double buffers: at the end of tile t the register
+// ring stores K(t+2) (into K(t)'s buffer, last read while S(t) was formed during tile t-1) and
+// V(t+1) (into V(t-1)'s), then issues the global loads of K(t+3) and V(t+2); one barrier a tile.
+// Same math, masking, defer-max and dropout as attn_fwd_kernel.
+template <int D, int OCC, int BN>
+__global__ void __launch_bounds__(256, OCC) attn_fwd_pipe_kernel(FwdArgs a) {
+  constexpr int KP = D + 8, VP = D + 32, NC = D / 16, NDB = D / 32, NKB = BN / 32;
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * VP];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, r = lane & 31;
+  int tx, ty;
+  xcd_tile(tx, ty);
+  const int bh = ty, b = bh / a.H, h = bh % a.H;
+  const int S = a.S;
+  const int qblk = tx * 128, q0 = qblk + w * 32;
+  const int q = q0 + r;
+  const bool qvalid = q < S;
+  const float sl2 = a.slopes ? a.slopes[h] * kLog2e : 0.f;
+  const float sc2 = a.scale * kLog2e;
+  const bool drop = a.maskA != nullptr;
+  const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
+  const RowSrc ksrc = row_src<D>(a.k + (size_t)b * S * a.ld + h * D, a.ld, S);
+  const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
+  const WordSrc wsrc = word_src(drop ? a.maskA + (size_t)bh * a.W * S : nullptr, a.lse, a.W, S, qvalid ? q : 0);
+
+  bf16x8 qf[NC];
+  {
+    const bf16* qp = a.q + ((size_t)(b * S + (qvalid ? q : 0)) * a.ld + h * D);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) qf[c] = qvalid ? *reinterpret_cast<const bf16x8*>(qp + 16 * c + 8 * hh) : bf16x8{};
+  }
+  f32x16 oacc[NDB];
+#pragma unroll
+  for (int d = 0; d < NDB; ++d) oacc[d] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  const int kend = a.causal ? min(S, qblk + 128) : S;
+  const int nt = (kend + BN - 1) / BN;
+  const int last = nt - 1;
+  TileLoader<D, BN> kl, vl;
+  uint32_t mwc[NKB], mwn[NKB];
+  auto load_words = [&](int k0, uint32_t* out) {
+#pragma unroll
+    for (int j = 0; j < NKB; ++j) out[j] = wsrc.load((k0 >> 5) + j);
+  };
+  // prologue: K(0), V(0), K(1) to LDS; the ring then holds K(2), V(1) and the keep words of tile 1
+  {
+    TileLoader<D, BN> k1l;
+    load_words(0, mwc);
+    kl.load(ksrc, 0);
+    vl.load(vsrc, 0);
+    k1l.load(ksrc, min(1, last) * BN);
+    kl.store(Ks[0], KP);
+    vl.store(Vs[0], VP);
+    k1l.store(Ks[1], KP);
+  }
+  kl.load(ksrc, min(2, last) * BN);
+  vl.load(vsrc, min(1, last) * BN);
+  load_words(min(1, last) * BN, mwn);
+  __syncthreads();
+
+  // score MFMAs of key block kb (32 keys) of a K tile
+  auto scores_kb = [&](const bf16* K, f32x16 (&sacc)[NKB], int kb) {
+    f32x16 acc = f32x16{};
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      acc = mfma32(*reinterpret_cast<const bf16x8*>(&K[(kb * 32 + r) * KP + 16 * c + 8 * hh]), qf[c], acc);
+    sacc[kb] = acc;
+  };
+  // Tile t: softmax of `cur` and O += V(t)^T P(t)^T, with the score MFMAs of the next K tile
+  // (Knext -> nxt) placed in the same basic blocks as the VALU work: key block 0 beside the row
+  // max, key block 1 beside exp / sums / dropout.  On the last tile Knext is a stale buffer and
+  // nxt is never read (unconditional issue keeps the MFMAs in the softmax's blocks).
+  auto tile_step = [&](f32x16 (&cur)[NKB], f32x16 (&nxt)[NKB], const bf16* Knext, int t) {
+    const int k0 = t * BN;
+    const bf16* V = Vs[t & 1];
+    const bool needmask = (k0 + BN > S) || (a.causal && k0 + BN - 1 > q0);
+    const bool slow = needmask || sl2 != 0.f;
+    float tmax = -INFINITY;
+    scores_kb(Knext, nxt, 0);
+    if (slow) {
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = k0 + kb * 32 + crow(i, hh);
+          float sv = fmaf(cur[kb][i], sc2, sl2 * (float)key);
+          if (needmask && (key >= S || (a.causal && key > q))) sv = -INFINITY;
+          cur[kb][i] = sv;
+          tmax = fmaxf(tmax, sv);
+        }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, cur[kb][i]);
+      tmax *= sc2;
+    }
+    tmax = xhalf_max(tmax);
+    if (!__all(tmax - m <= a.thr)) {
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = m == -INFINITY ? 0.f : fexp2(m - mnew);
+      m = mnew;
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) oacc[d] *= alpha;
+    }
+    scores_kb(Knext, nxt, 1);
+    const float mexp = m == -INFINITY ? 0.f : m;
+    const float msc = slow ? 1.f : sc2;
+    float ps[4];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pv = fexp2(fmaf(cur[kb][i], msc, -mexp));
+        ps[i & 3] = (kb == 0 && i < 4) ? pv : ps[i & 3] + pv;
+        cur[kb][i] = pv;
+      }
+    l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+    if (drop) {
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        const uint32_t mw = half_word(mwc[kb], hh);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) cur[kb][i] = keep_bits(cur[kb][i], mw, crow(i, 0));
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (bf16)cur[kb][8 * s2 + j];
+#pragma unroll
+        for (int d = 0; d < NDB; ++d) oacc[d] = mfma32(tr_operand(V, VP, kb * 32 + 16 * s2, d * 32, lane), pf, oacc[d]);
+      }
+    // end of tile t: K(t+2), V(t+1) from the ring into LDS, next loads, one barrier
+    if (t + 1 < nt) {
+      if (t + 2 < nt) kl.store(Ks[t & 1], KP);
+      vl.store(Vs[(t + 1) & 1], VP);
+#pragma unroll
+      for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
+      kl.load(ksrc, min(t + 3, last) * BN);     // clamped: a harmless reload keeps the issue unconditional
+      vl.load(vsrc, min(t + 2, last) * BN);
+      load_words(min(t + 2, last) * BN, mwn);
+    }
+    __syncthreads();
+  };
+  f32x16 sA[NKB], sB[NKB];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) scores_kb(Ks[0], sA, kb);
+  for (int t = 0; t < nt; t += 2) {
+    tile_step(sA, sB, Ks[1], t);                 // K(t+1) is in Ks[(t+1) & 1]
+    if (t + 1 < nt) tile_step(sB, sA, Ks[0], t + 1);
+  }
+  l = xhalf_sum(l);
+  if (!qvalid) return;
+  const float inv_l = l > 0.f ? inv_keep / l : 0.f;
+  bf16* op = a.o + (size_t)(b * S + q) * a.ldo + h * D;
+#pragma unroll
+  for (int d = 0; d < NDB; ++d)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      bf16x4 v4;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v4[t] = (bf16)(oacc[d][4 * gq + t] * inv_l);
+      *reinterpret_cast<bf16x4*>(op + d * 32 + 8 * gq + 4 * hh) = v4;
+    }
+  if (hh == 0) a.lse[(size_t)bh * S + q] = (m + log2f(l)) * kLn2;
+}
+
 struct BwdArgs {
   const bf16* q; const bf16* k; const bf16* v; const bf16* dout; const float* lse; float* delta;
   const bf16* o;   // forward output: the dQ kernel forms delta = rowsum(dO * O) from it
@@ -564,7 +786,8 @@ __device__ __forceinline__ int colsum_col(int k, int hh) { return (k >> 4) * 32 
 // merges cost 16 v_mov per query sub-block) and no bias add without ALiBi.
 template <int D, int OCC, int BM, bool DROP, bool ALIBI>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
-  constexpr int QP = D + 8, NC = D / 16, NDB = D / 32;
+  constexpr bool SWZ = D == 64;                 // swizzled unpadded image (swz64_off)
+  constexpr int QP = SWZ ? D : D + 8, NC = D / 16, NDB = D / 32;
   // One LDS block, row statistics first: placed after the 72 KiB of Q/dO tiles (BM = 128) their
   // ds_read offsets exceed the 16-bit immediate and every read needed a VALU address add.
   struct Smem {
@@ -636,8 +859,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   ol.load(osrc, qstart);
   load_stats(qstart);
   load_words(qstart, mwc);
-  ql.store(Qs[0], QP);
-  ol.store(Os[0], QP);
+  ql.store_bwd(Qs[0], QP);
+  ol.store_bwd(Os[0], QP);
   if (threadIdx.x < BM) { lse_s[0][threadIdx.x] = lse_r; del_s[0][threadIdx.x] = del_r; }
   __syncthreads();
   for (int t = 0; t < nt; ++t) {
@@ -659,8 +882,13 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       f32x16 sacc = f32x16{}, pacc = f32x16{};
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        sacc = mfma32(*reinterpret_cast<const bf16x8*>(&Q[(qb * 32 + r) * QP + 16 * c + 8 * hh]), kf[c], sacc);
-        pacc = mfma32(*reinterpret_cast<const bf16x8*>(&O[(qb * 32 + r) * QP + 16 * c + 8 * hh]), vf[c], pacc);
+        if constexpr (SWZ) {
+          sacc = mfma32(swz_row_read(Q, qb * 32, r, 2 * c + hh), kf[c], sacc);
+          pacc = mfma32(swz_row_read(O, qb * 32, r, 2 * c + hh), vf[c], pacc);
+        } else {
+          sacc = mfma32(*reinterpret_cast<const bf16x8*>(&Q[(qb * 32 + r) * QP + 16 * c + 8 * hh]), kf[c], sacc);
+          pacc = mfma32(*reinterpret_cast<const bf16x8*>(&O[(qb * 32 + r) * QP + 16 * c + 8 * hh]), vf[c], pacc);
+        }
       }
       const int qrow0 = q0 + qb * 32;
       // block-uniform predicate (a scalar branch, never a per-element one)
@@ -720,14 +948,19 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
         for (int j = 0; j < 8; ++j) { pb[j] = (bf16)sacc[8 * s + j]; sb[j] = (bf16)pacc[8 * s + j]; }
 #pragma unroll
         for (int d = 0; d < NDB; ++d) {
-          dv[d] = mfma32(tr_operand(O, QP, qb * 32 + 16 * s, d * 32, lane), pb, dv[d]);
-          dk[d] = mfma32(tr_operand(Q, QP, qb * 32 + 16 * s, d * 32, lane), sb, dk[d]);
+          if constexpr (SWZ) {
+            dv[d] = mfma32(tr_operand_swz(O, qb * 32 + 16 * s, d * 32, lane), pb, dv[d]);
+            dk[d] = mfma32(tr_operand_swz(Q, qb * 32 + 16 * s, d * 32, lane), sb, dk[d]);
+          } else {
+            dv[d] = mfma32(tr_operand(O, QP, qb * 32 + 16 * s, d * 32, lane), pb, dv[d]);
+            dk[d] = mfma32(tr_operand(Q, QP, qb * 32 + 16 * s, d * 32, lane), sb, dk[d]);
+          }
         }
       }
     }
     if (t + 1 < nt) {
-      ql.store(Qs[buf ^ 1], QP);
-      ol.store(Os[buf ^ 1], QP);
+      ql.store_bwd(Qs[buf ^ 1], QP);
+      ol.store_bwd(Os[buf ^ 1], QP);
       if (threadIdx.x < BM) { lse_s[buf ^ 1][threadIdx.x] = lse_r; del_s[buf ^ 1][threadIdx.x] = del_r; }
 #pragma unroll
       for (int j = 0; j < NQW; ++j) mwc[j] = mwn[j];
@@ -769,7 +1002,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
 // registers -- no atomics, no cross-workgroup reduction.
 template <int D, int OCC, int BN, int RING>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
-  constexpr int KP = D + 8, NC = D / 16, NDB = D / 32;
+  constexpr bool SWZ = D == 64;                 // swizzled unpadded K / V images (swz64_off)
+  constexpr int KP = SWZ ? D : D + 8, NC = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * KP];
 
@@ -838,8 +1072,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   load_words(0, mwc);
   kl0.load(ksrc, 0);
   vl0.load(vsrc, 0);
-  kl0.store(Ks[0], KP);
-  vl0.store(Vs[0], KP);
+  kl0.store_bwd(Ks[0], KP);
+  vl0.store_bwd(Vs[0], KP);
   {
     const int k1 = min(1, nt - 1) * BN, k2 = min(2, nt - 1) * BN;
     kl1.load(ksrc, k1); vl1.load(vsrc, k1); load_words(k1, mw1);
@@ -860,8 +1094,13 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
       f32x16 sacc = f32x16{}, pacc = f32x16{};
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        sacc = mfma32(*reinterpret_cast<const bf16x8*>(&K[(kb * 32 + r) * KP + 16 * c + 8 * hh]), qf[c], sacc);
-        pacc = mfma32(*reinterpret_cast<const bf16x8*>(&V[(kb * 32 + r) * KP + 16 * c + 8 * hh]), of[c], pacc);
+        if constexpr (SWZ) {
+          sacc = mfma32(swz_row_read(K, kb * 32, r, 2 * c + hh), qf[c], sacc);
+          pacc = mfma32(swz_row_read(V, kb * 32, r, 2 * c + hh), of[c], pacc);
+        } else {
+          sacc = mfma32(*reinterpret_cast<const bf16x8*>(&K[(kb * 32 + r) * KP + 16 * c + 8 * hh]), qf[c], sacc);
+          pacc = mfma32(*reinterpret_cast<const bf16x8*>(&V[(kb * 32 + r) * KP + 16 * c + 8 * hh]), of[c], pacc);
+        }
       }
       const uint32_t mw = half_word(mwc[kb], hh);
       // P = exp2(s*log2e - lse): 2 VALU on interior tiles without ALiBi
@@ -891,12 +1130,15 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) sb[j] = (bf16)sacc[8 * s + j];
 #pragma unroll
-        for (int d = 0; d < NDB; ++d) dq[d] = mfma32(tr_operand(K, KP, kb * 32 + 16 * s, d * 32, lane), sb, dq[d]);
+        for (int d = 0; d < NDB; ++d) {
+          if constexpr (SWZ) dq[d] = mfma32(tr_operand_swz(K, kb * 32 + 16 * s, d * 32, lane), sb, dq[d]);
+          else dq[d] = mfma32(tr_operand(K, KP, kb * 32 + 16 * s, d * 32, lane), sb, dq[d]);
+        }
       }
     }
     if (t + 1 < nt) {
-      kn.store(Ks[buf ^ 1], KP);
-      vn.store(Vs[buf ^ 1], KP);
+      kn.store_bwd(Ks[buf ^ 1], KP);
+      vn.store_bwd(Vs[buf ^ 1], KP);
 #pragma unroll
       for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
       // tile t+1+RING (clamped to the last tile: a harmless reload keeps the issue unconditional)
@@ -951,6 +1193,13 @@ static int occupancy(int which) {
   return v[which];
 }
 
+// Forward form (D = 64): DTD_ATTN_FWD=pipe selects attn_fwd_pipe_kernel (S(t+1) MFMAs under
+// tile t's softmax); anything else the single-stage attn_fwd_kernel.
+static bool fwd_pipe() {
+  const char* e = getenv("DTD_ATTN_FWD");
+  return e != nullptr && strcmp(e, "pipe") == 0;
+}
+
 // Keys per K/V tile of the dQ kernel (which=1; the forward uses 64): 64 (37 KB LDS) or 128
 // (74 KB LDS; half the barriers per key, but 2 waves/SIMD at most).  64 with the 3-wave kernel
 // (128-key dQ at 2 waves: 3 % slower backward).  Measured and dropped: 128-key forward tiles
@@ -996,7 +1245,10 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
   FwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, slopes, mA, B, S, H, ld, ldo, causal, W,
             scale, p, thr};
   dim3 grid((S + 127) / 128, B * H);
-  if (D == 64) {
+  if (D == 64 && fwd_pipe()) {
+    // two score tiles live: 198 VGPRs, 2 waves / SIMD (at 3 it spills)
+    hipLaunchKernelGGL((attn_fwd_pipe_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
+  } else if (D == 64) {
     const int o = occupancy(0);
     if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
     else if (o == 2) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 64, 2>), grid, dim3(256), 0, s, a);

@@ -30,8 +30,10 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("fwd", ["single", "pipe"])
 @pytest.mark.parametrize("B,S,H,D,causal,alibi,p", CASES)
-def test_flash_attention_fwd_bwd(B, S, H, D, causal, alibi, p):
+def test_flash_attention_fwd_bwd(B, S, H, D, causal, alibi, p, fwd, monkeypatch):
+    monkeypatch.setenv("DTD_ATTN_FWD", fwd)
     torch.manual_seed(0)
     qkv = torch.randn(B * S, 3 * H * D).to(torch.bfloat16)
     dctx = torch.randn(B * S, H * D).to(torch.bfloat16)
@@ -56,6 +58,23 @@ def test_flash_attention_fwd_bwd(B, S, H, D, causal, alibi, p):
     assert torch.equal(dq_b, dq_g)
     ref_db = dq_g.float().sum(0)
     assert ((db - 0.25) - ref_db).abs().max().item() <= 1e-3 * (ref_db.abs().max().item() + 1.0)
+
+
+@pytest.mark.parametrize("B,S,H,D,causal,alibi,p", [c for c in CASES if c[3] == 64] + [(4, 512, 12, 64, False, False, 0.1)])
+def test_pipelined_forward_is_bitwise_the_single_stage_forward(B, S, H, D, causal, alibi, p, monkeypatch):
+    """attn_fwd_pipe_kernel (next tile's score MFMAs under this tile's softmax) reorders issue,
+    not arithmetic: output and LSE equal attn_fwd_kernel's bit for bit."""
+    torch.manual_seed(3)
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda").to(torch.bfloat16)
+    slopes = A.alibi_slopes(H).cuda() if alibi else None
+    outs = {}
+    for fwd in ("single", "pipe"):
+        monkeypatch.setenv("DTD_ATTN_FWD", fwd)
+        rg = RngState(17, device="cuda")
+        outs[fwd] = A.attn_fwd(qkv, B, S, H, D, causal, slopes, p, rg, 2)
+    torch.cuda.synchronize()
+    assert torch.equal(outs["single"][0], outs["pipe"][0])
+    assert torch.equal(outs["single"][1], outs["pipe"][1])
 
 
 def test_side_stream_masks_match_inline_generation():
@@ -95,11 +114,13 @@ def _fwd_fp64(qkv, B, S, H, D, causal):
     return ctx.transpose(1, 2).reshape(B * S, H * D), lse
 
 
+@pytest.mark.parametrize("fwd", ["single", "pipe"])
 @pytest.mark.parametrize("causal", [False, True])
-def test_defer_max_rescale_branch_forced(monkeypatch, causal):
+def test_defer_max_rescale_branch_forced(monkeypatch, causal, fwd):
     """SKILL rule 26: the defer-max rescale is data dependent.  Force it at chosen tiles (and a
     sub-threshold growth in between), check the FULL output against an fp64 host reference,
     and check that the shipped threshold and THR=0 (rescale on every growth) agree."""
+    monkeypatch.setenv("DTD_ATTN_FWD", fwd)
     B, S, H, D = 2, 512, 2, 64
     qkv = _spiked_qkv(B, S, H, D, [(70, 1.0), (200, 1.5), (330, 2.5), (460, 2.6)])
     ref_ctx, ref_lse = _fwd_fp64(qkv, B, S, H, D, causal)
