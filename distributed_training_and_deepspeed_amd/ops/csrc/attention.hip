@@ -371,7 +371,9 @@ struct TileLoader {
 
 // grid: (ceil(S/128), B*H); block 256 = 4 waves x 32 queries.  KV tiles of BN keys,
 // double-buffered in LDS, fed by a 2-deep register ring of global loads: one barrier per tile.
-template <int D, int OCC, int BN, int RING>
+// PK: the exp-argument FMAs and the row-sum adds as packed fp32 (v_pk_fma_f32 / v_pk_add_f32, two
+// scores per issue) -- 32 fewer VALU issues per 64-key tile; the row sum's add order differs.
+template <int D, int OCC, int BN, int RING, bool PK = false>
 __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   // K rows (ds_read_b128, 4x16-lane groups): pitch D+8 puts the 16 rows of a group on 16
   // distinct 4-bank windows.  V (ds_read_b64_tr_b16, rows rr = 0..3 x column halves g = 0,1 per
@@ -495,16 +497,33 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     const float msc = slow ? 1.f : sc2;
     // l stays a per-half partial (both halves share m, hence every rescale); the two halves
     // are combined once in the epilogue.  Four independent partial sums shorten the add chain.
-    float ps[4];
+    if constexpr (PK) {
+      const f32x2 msc2 = pk2(msc, msc), nm2 = pk2(-mexp, -mexp);
+      f32x2 ps2[2];
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
+      for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float pv = fexp2(fmaf(sacc[kb][i], msc, -mexp));
-        ps[i & 3] = (kb == 0 && i < 4) ? pv : ps[i & 3] + pv;   // no "+ 0" adds (-0 semantics keep them)
-        sacc[kb][i] = pv;
-      }
-    l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+        for (int i = 0; i < 16; i += 2) {
+          const f32x2 x = pk_fma(pk2(sacc[kb][i], sacc[kb][i + 1]), msc2, nm2);
+          const f32x2 pv = pk2(fexp2(x.x), fexp2(x.y));
+          const int j = (i >> 1) & 1;
+          ps2[j] = (kb == 0 && i < 4) ? pv : ps2[j] + pv;
+          sacc[kb][i] = pv.x;
+          sacc[kb][i + 1] = pv.y;
+        }
+      l += (ps2[0].x + ps2[0].y) + (ps2[1].x + ps2[1].y);
+    } else {
+      float ps[4];
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float pv = fexp2(fmaf(sacc[kb][i], msc, -mexp));
+          ps[i & 3] = (kb == 0 && i < 4) ? pv : ps[i & 3] + pv;   // no "+ 0" adds (-0 semantics keep them)
+          sacc[kb][i] = pv;
+        }
+      l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+    }
     if (drop) {
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
@@ -1000,7 +1019,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
 // dQ: grid (ceil(S/128), B*H); block 256 = 4 waves x 32 queries (query on the lane, as in the
 // forward); recomputes S^T and dP^T per 64-key tile and accumulates dQ^T = K^T.dS^T in
 // registers -- no atomics, no cross-workgroup reduction.
-template <int D, int OCC, int BN, int RING>
+// PK: packed-fp32 exp arguments and dS = P (dP - delta) (v_pk_fma_f32 / v_pk_mul_f32)
+template <int D, int OCC, int BN, int RING, bool PK = false>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   constexpr bool SWZ = D == 64;                 // swizzled unpadded K / V images (swz64_off)
   constexpr int KP = SWZ ? D : D + 8, NC = D / 16, NDB = D / 32;
@@ -1112,12 +1132,30 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
           if (needmask && (!qvalid || key >= S || (a.causal && key > q))) pv = 0.f;
           sacc[i] = pv;
         }
+      } else if constexpr (PK) {
+        const f32x2 sc22 = pk2(sc2, sc2), nl2 = pk2(-lse2, -lse2);
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          const f32x2 x = pk_fma(pk2(sacc[i], sacc[i + 1]), sc22, nl2);
+          sacc[i] = fexp2(x.x);
+          sacc[i + 1] = fexp2(x.y);
+        }
       } else {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[i] = fexp2(fmaf(sacc[i], sc2, -lse2));
       }
       // dS^T = P * (dP - delta), dP = dropout(dP') (keep bit, 1/(1-p))
-      if (drop) {
+      if constexpr (PK) {
+        const f32x2 ik2 = pk2(drop ? inv_keep : 1.f, drop ? inv_keep : 1.f), nd2 = pk2(-dl, -dl);
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          f32x2 dp = pk2(pacc[i], pacc[i + 1]);
+          if (drop) dp = pk2(keep_bits(pacc[i], mw, crow(i, 0)), keep_bits(pacc[i + 1], mw, crow(i + 1, 0)));
+          const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * pk_fma(dp, ik2, nd2);
+          sacc[i] = ds.x;
+          sacc[i + 1] = ds.y;
+        }
+      } else if (drop) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[i] *= fmaf(keep_bits(pacc[i], mw, crow(i, 0)), inv_keep, -dl);
       } else {
@@ -1200,6 +1238,12 @@ static bool fwd_pipe() {
   return e != nullptr && strcmp(e, "pipe") == 0;
 }
 
+// DTD_ATTN_FWD_PK=1: the packed-fp32 softmax forms of attn_fwd_kernel and attn_bwd_dq_kernel (PK)
+static bool fwd_pk() {
+  const char* e = getenv("DTD_ATTN_FWD_PK");
+  return e != nullptr && e[0] == '1';
+}
+
 // Keys per K/V tile of the dQ kernel (which=1; the forward uses 64): 64 (37 KB LDS) or 128
 // (74 KB LDS; half the barriers per key, but 2 waves/SIMD at most).  64 with the 3-wave kernel
 // (128-key dQ at 2 waves: 3 % slower backward).  Measured and dropped: 128-key forward tiles
@@ -1250,7 +1294,8 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
     hipLaunchKernelGGL((attn_fwd_pipe_kernel<64, 2, 64>), grid, dim3(256), 0, s, a);
   } else if (D == 64) {
     const int o = occupancy(0);
-    if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
+    if (o >= 3 && fwd_pk()) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64, 1, true>), grid, dim3(256), 0, s, a);
+    else if (o >= 3) hipLaunchKernelGGL((attn_fwd_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
     else if (o == 2) hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 64, 2>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_fwd_kernel<64, 1, 64, 2>), grid, dim3(256), 0, s, a);
   } else if (D == 128) {
@@ -1302,6 +1347,7 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   if (D == 64) {
     const int o = occupancy(2);
     if (tile_keys(1) == 128) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 128, 2>), grid, dim3(256), 0, s, a);
+    else if (o >= 3 && fwd_pk()) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 64, 1, true>), grid, dim3(256), 0, s, a);
     else if (o >= 3) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 3, 64, 1>), grid, dim3(256), 0, s, a);
     else if (o == 2) hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 2, 64, 2>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, 1, 64, 2>), grid, dim3(256), 0, s, a);

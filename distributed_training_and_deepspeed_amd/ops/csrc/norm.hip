@@ -154,15 +154,29 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
   const uint32_t thr = keep_threshold(a.p);
   const float scale = has_drop ? 1.f / (1.f - a.p) : 1.f;
   float pg[NPL], pb[NPL], py[NPL];
-  // gamma / beta stay packed (bf16: VEC / 2 registers per chunk) and are widened at each use.
-  // FO: they are re-read (L1 / L2 hits) with each row's loads -- the compiler barrier in front
-  // stops hipcc from hoisting 2 x NPL widened loop invariants into registers (4 -> 3 waves / SIMD)
-  vt gmr[ITERS], btr[FO ? ITERS : 1];
+  // LDS: FO's per-column constants during the row loop, the column-partial reduction after it
+  __shared__ __attribute__((aligned(16))) float sh[4][2048];  // nw <= 4 waves, h <= 2048
+  // non-FO: gamma stays packed (bf16: VEC / 2 registers per chunk) and is widened at each use.
+  // FO: gamma, beta and 1/gamma as fp32 columns in LDS, re-read (ds_read_b128) for every row --
+  // the compiler barrier at the top of each row stops hipcc from hoisting them as 3 x NPL loop
+  // invariants into registers (4 -> 3 waves / SIMD: measured slower than the extra LDS reads)
+  vt gmr[FO ? 1 : ITERS];
+  float* const cg = &sh[0][0];
+  float* const cb = cg + h;
+  float* const cr = cb + h;
 #pragma unroll
   for (int i = 0; i < NPL; ++i) { pg[i] = 0.f; pb[i] = 0.f; py[i] = 0.f; }
   if constexpr (!FO) {
 #pragma unroll
     for (int c = 0; c < ITERS; ++c) gmr[c] = ld_raw<T, VEC, 0>((const T*)a.gamma + (c * LPR + sub) * VEC);
+  } else {
+    for (int col = threadIdx.x; col < h; col += blockDim.x) {
+      const float gv = (float)((const T*)a.gamma)[col];
+      cg[col] = gv;
+      cb[col] = (float)((const T*)a.beta)[col];
+      cr[col] = safe_rcp(gv);
+    }
+    __syncthreads();
   }
   const T* src = (const T*)(FO ? a.xo : a.z);
   const bool two = a.dout2 != nullptr;
@@ -171,14 +185,6 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
   float nmu = 0.f, nrs = 0.f;
   auto fetch = [&](int r) {
     const size_t b = (size_t)r * h;
-    if constexpr (FO) {
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int c = 0; c < ITERS; ++c) {
-        gmr[c] = ld_raw<T, VEC, 0>((const T*)a.gamma + (c * LPR + sub) * VEC);
-        btr[c] = ld_raw<T, VEC, 0>((const T*)a.beta + (c * LPR + sub) * VEC);
-      }
-    }
 #pragma unroll
     for (int c = 0; c < ITERS; ++c) {
       const int col = (c * LPR + sub) * VEC;
@@ -193,6 +199,7 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
   if (PF && row < a.rows) fetch(row);
   for (; row < a.rows; row += stride) {
     const size_t base = (size_t)row * h;
+    if constexpr (FO) asm volatile("" ::: "memory");
     if (!PF) fetch(row);
     vt cz[ITERS], cd[ITERS], ce[ITERS];
 #pragma unroll
@@ -213,9 +220,15 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         const int i = c * VEC + j;
-        const float gmv = (float)gmr[c][j];
-        if constexpr (FO) xh[i] = (zz[j] - (float)btr[c][j]) * safe_rcp(gmv);
-        else xh[i] = (zz[j] - mu) * rs;
+        float gmv;
+        if constexpr (FO) {
+          const int col = (c * LPR + sub) * VEC + j;
+          gmv = cg[col];
+          xh[i] = (zz[j] - cb[col]) * cr[col];
+        } else {
+          gmv = (float)gmr[c][j];
+          xh[i] = (zz[j] - mu) * rs;
+        }
         dg[i] = dd[j] * gmv;
         s1 += dg[i];
         s2 += dg[i] * xh[i];
@@ -251,8 +264,8 @@ __global__ void __launch_bounds__(256) ln_bwd_wave(LnBwdArgs a) {
       }
     }
   }
-  // Block-level reduction of the column partials through LDS (one array at a time).
-  __shared__ float sh[4][2048];  // nw <= 4 waves, h <= 2048
+  // Block-level reduction of the column partials through LDS (one array at a time; the first
+  // barrier also retires every wave's reads of FO's constants)
   float* outs[3] = {a.part_gamma, a.part_beta, a.part_bias};
   float* srcs[3] = {pg, pb, py};
 #pragma unroll

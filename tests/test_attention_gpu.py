@@ -30,10 +30,17 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("fwd", ["single", "pipe"])
+def _form(monkeypatch, fwd):
+    """single: attn_fwd_kernel; pipe: attn_fwd_pipe_kernel; pk: packed-fp32 softmax forms of the
+    forward and dQ kernels."""
+    monkeypatch.setenv("DTD_ATTN_FWD", "pipe" if fwd == "pipe" else "single")
+    monkeypatch.setenv("DTD_ATTN_FWD_PK", "1" if fwd == "pk" else "0")
+
+
+@pytest.mark.parametrize("fwd", ["single", "pipe", "pk"])
 @pytest.mark.parametrize("B,S,H,D,causal,alibi,p", CASES)
 def test_flash_attention_fwd_bwd(B, S, H, D, causal, alibi, p, fwd, monkeypatch):
-    monkeypatch.setenv("DTD_ATTN_FWD", fwd)
+    _form(monkeypatch, fwd)
     torch.manual_seed(0)
     qkv = torch.randn(B * S, 3 * H * D).to(torch.bfloat16)
     dctx = torch.randn(B * S, H * D).to(torch.bfloat16)
@@ -114,13 +121,13 @@ def _fwd_fp64(qkv, B, S, H, D, causal):
     return ctx.transpose(1, 2).reshape(B * S, H * D), lse
 
 
-@pytest.mark.parametrize("fwd", ["single", "pipe"])
+@pytest.mark.parametrize("fwd", ["single", "pipe", "pk"])
 @pytest.mark.parametrize("causal", [False, True])
 def test_defer_max_rescale_branch_forced(monkeypatch, causal, fwd):
     """SKILL rule 26: the defer-max rescale is data dependent.  Force it at chosen tiles (and a
     sub-threshold growth in between), check the FULL output against an fp64 host reference,
     and check that the shipped threshold and THR=0 (rescale on every growth) agree."""
-    monkeypatch.setenv("DTD_ATTN_FWD", fwd)
+    _form(monkeypatch, fwd)
     B, S, H, D = 2, 512, 2, 64
     qkv = _spiked_qkv(B, S, H, D, [(70, 1.0), (200, 1.5), (330, 2.5), (460, 2.6)])
     ref_ctx, ref_lse = _fwd_fp64(qkv, B, S, H, D, causal)
