@@ -674,7 +674,10 @@ __device__ __forceinline__ void sched_finish(int* q, int nwg, int tid) {
 template <int EPI, bool DYN>
 __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // the wave index through readfirstlane: provably uniform, so the LDS-DMA destinations (M0) are
+  // formed with scalar adds instead of a v_readfirstlane per DMA (-11 % VALU; +2-3 % vs hipBLASLt
+  // on the BERT projection shapes, profiles/r3_gemm_u2_experiment.jsonl)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lq = lane >> 4, sw = li & 7;
   const int wm = w >> 2, wn = w & 3;
   const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn;

@@ -557,3 +557,83 @@ __global__ void __launch_bounds__(256, 1) gemm_bt_w4(GemmArgs g) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// "U2" (DTD_GEMM_VARIANT 2, removed): gemm_bt_persistent's K-step loop unrolled by two (K / 64
+// even) so each K-step's LDS buffer is a compile-time constant, every K-step stages (the
+// workgroup's last one a duplicate of its tile's K-step 0, drained before exit) so the phases have
+// one counted vmcnt and no staging branch.  The constant-buffer fragment addressing needs more
+// live address registers: 256 VGPRs with 14-20 spilled INTO the main loop -> 0.74-0.83x v1
+// (profiles/r3_gemm_u2_experiment.jsonl).  A layout with both buffers' A (and B) halves within
+// one 16-bit ds_read offset of a single base ([A0][A1][B0][B1]) would be the way to retry it.
+// The K-step body, as it was written (a macro inside gemm_bt_persistent, CB = buffer, FIRST =
+// first K-step after an epilogue):
+// // One K-step of the U2 main loop (reads LDS buffer CB, stages the next K-step into the other);
+// // used inside gemm_bt_persistent only
+// #define DTD_KSTEP(CB, FIRST, KT_)                                                           \
+//   do {                                                                                      \
+//     constexpr bool first = (FIRST);                                                         \
+//     const int kt = (KT_);                                                                   \
+//     const char* cur = smem + (CB) * TILE_BYTES; \
+//     char* nxt = smem + ((CB) ^ 1) * TILE_BYTES; \
+//     const bool more_here = kt + 1 < nk; \
+//     const auto sra = more_here ? rsa : (has_next ? rsa1 : rsa); \
+//     const auto srb = more_here ? rsb : (has_next ? rsb1 : rsb); \
+//     const int skt = more_here ? kt + 1 : 0; \
+//     _Pragma("unroll")                                                                      \
+//     for (int p = 0; p < 4; ++p) { \
+//       if (p == 0 || p == 2) { \
+//         const int qm = p == 0 ? 0 : 1; \
+//     _Pragma("unroll")                                                                      \
+//         for (int mi = 0; mi < 4; ++mi) { \
+//           const char* rr = cur + arow + (qm * 4 + mi) * 16 * 128; \
+//           af[mi][0] = *reinterpret_cast<const bf16x8*>(rr + ch0); \
+//           af[mi][1] = *reinterpret_cast<const bf16x8*>(rr + ch1); \
+//         } \
+//       } \
+//       if (p == 0 || p == 1) { \
+//     _Pragma("unroll")                                                                      \
+//         for (int ni = 0; ni < 2; ++ni) { \
+//           const char* rr = cur + brow + (p * 2 + ni) * 16 * 128; \
+//           bf16x8 x0 = *reinterpret_cast<const bf16x8*>(rr + ch0); \
+//           bf16x8 x1 = *reinterpret_cast<const bf16x8*>(rr + ch1); \
+//           if (p == 0) { b0[ni][0] = x0; b0[ni][1] = x1; } else { b1[ni][0] = x0; b1[ni][1] = x1; } \
+//         } \
+//       } \
+//       if (p == 0) stage<0>(so, sra, srb, nxt, skt); \
+//       if (p == 1) stage<1>(so, sra, srb, nxt, skt); \
+//       if (p == 2) stage<2>(so, sra, srb, nxt, skt); \
+//       if (p == 3) stage<3>(so, sra, srb, nxt, skt); \
+//       if (first && p < 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WAIT_FIRST) : "memory"); \
+//       else asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); \
+//       bar(); \
+//       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+//       __builtin_amdgcn_sched_barrier(0); \
+//       __builtin_amdgcn_s_setprio(1); \
+//       const int qm = (p == 2 || p == 3) ? 1 : 0; \
+//     _Pragma("unroll")                                                                      \
+//       for (int mi = 0; mi < 4; ++mi) \
+//     _Pragma("unroll")                                                                      \
+//         for (int ni = 0; ni < 2; ++ni) \
+//     _Pragma("unroll")                                                                      \
+//           for (int ks = 0; ks < 2; ++ks) { \
+//             const bf16x8 bb = (p == 1 || p == 2) ? b1[ni][ks] : b0[ni][ks]; \
+//             const int nn = ((p == 1 || p == 2) ? 2 : 0) + ni; \
+//             acc[qm * 4 + mi][nn] = mfma16(bb, af[mi][ks], acc[qm * 4 + mi][nn]); \
+//           } \
+//       __builtin_amdgcn_s_setprio(0); \
+//       bar(); \
+//     } \
+//   } while (0)
+// 
+//     if constexpr (U2) {
+//       // K-step kt reading buffer CB; `first` (compile-time) selects the waits that also cover the
+//       // previous tile's epilogue stores
+//       DTD_KSTEP(0, true, 0);
+//       DTD_KSTEP(1, false, 1);
+//       for (int kt2 = 2; kt2 < nk; kt2 += 2) {
+//         DTD_KSTEP(0, false, kt2);
+//         DTD_KSTEP(1, false, kt2 + 1);
+//       }
+//       buf = 0;   // the last K-step read buffer 1 (the epilogue's image); buffer 0 holds the next K-step 0
+//     } else {
