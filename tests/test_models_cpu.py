@@ -62,6 +62,30 @@ def test_post_ln_backward_with_and_without_stored_z(memeff, monkeypatch):
     test_fused_backward_matches_autograd("tiny", {})
 
 
+def test_ln_bwd_from_output_matches_stored_z_form():
+    """ops.functional.ln_bwd: x-hat recomputed from the LN output (memory-efficient form) gives the
+    stored-z gradients in fp32 on CPU; z=None without the output is refused."""
+    from distributed_training_and_deepspeed_amd.ops import functional as Fx
+    from distributed_training_and_deepspeed_amd.ops.rng import RngState
+    torch.manual_seed(0)
+    rows, h = 37, 64
+    y, r, dout, dout2 = (torch.randn(rows, h) for _ in range(4))
+    gamma, beta = 1 + 0.1 * torch.randn(h), 0.1 * torch.randn(h)
+    rng = RngState(3)
+    res = {}
+    for fo in (False, True):
+        z, o, m, rs = Fx.ln_fwd(y, r, gamma, beta, 1e-5, 0.1, rng, 7, store_z=not fo)
+        dg, db, dbias = (torch.zeros(h) for _ in range(3))
+        kw = dict(xout=o, beta=beta) if fo else {}
+        dz, dy = Fx.ln_bwd(dout, None, z, m, rs, gamma, 0.1, rng, 7, want_dz=True, want_dy=True, dgamma=dg,
+                           dbeta=db, dbias=dbias, dout2=dout2, **kw)
+        res[fo] = (dz, dy, dg, db, dbias)
+    for a, b in zip(res[False], res[True]):
+        assert torch.allclose(a, b, atol=1e-4, rtol=1e-4)
+    with pytest.raises(ValueError):
+        Fx.ln_bwd(dout, None, None, m, rs, gamma, 0.1, rng, 7)
+
+
 def test_mlm_masking_law():
     cfg = C.BERT_BASE
     ds = SyntheticLMDataset(cfg, 64, seq_len=512, seed=0)
