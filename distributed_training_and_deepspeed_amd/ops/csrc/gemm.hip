@@ -952,315 +952,6 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
   if constexpr (DYN) sched_finish(g.sched, nwg, tid);
 }
 
-// ---- split-buffer form (DTD_GEMM_VARIANT 2, K / 64 even) --------------------------------------
-// LDS as [A0 | A1 | B0 | B1] (32 KiB each) instead of [A0 B0 | A1 B1]: every fragment read of
-// either K-step buffer is then one per-lane base register + a 16-bit immediate (buffer 1 is +32
-// KiB), so the K-step loop can be unrolled by two with compile-time buffers and NO per-phase
-// address arithmetic; every K-step stages (the workgroup's last one a duplicate of its tile's
-// K-step 0, drained before exit), so each phase has one counted vmcnt and no staging branch.
-__device__ __forceinline__ StageOffs stage_offsets2(int w, int lane, int lda, int ldb) {
-  StageOffs o = stage_offsets(w, lane, lda, ldb);
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) o.lb[h][i] -= A_BYTES;   // B rows relative to their own half
-  return o;
-}
-template <int H>
-__device__ __forceinline__ void stage2(const StageOffs& o, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb,
-                                       char* abuf, char* bbuf, int kt) {
-  const int so = kt * BK * 2;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    if constexpr (H == 0 || H == 3) {
-      constexpr int h = H == 3 ? 1 : 0;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(abuf + o.la[h][i]), 16, o.a[h][i], so, 0, 0);
-    } else {
-      constexpr int h = H == 2 ? 1 : 0;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(bbuf + o.lb[h][i]), 16, o.b[h][i], so, 0, 0);
-    }
-  }
-}
-// one K-step of gemm_bt_persistent2: reads buffer CB, stages the next K-step into buffer CB ^ 1
-#define DTD_KSTEP2(CB, FIRST, KT_)                                                                  \
-  do {                                                                                             \
-    constexpr bool first = (FIRST);                                                                \
-    const int kt = (KT_);                                                                          \
-    const char* ca = smem + (CB) * A_BYTES;                                                         \
-    char* na = smem + ((CB) ^ 1) * A_BYTES;                                                         \
-    char* nb = smem + 2 * A_BYTES + ((CB) ^ 1) * A_BYTES;                                           \
-    const bool more_here = kt + 1 < nk;                                                            \
-    const auto sra = more_here ? rsa : (has_next ? rsa1 : rsa);                                     \
-    const auto srb = more_here ? rsb : (has_next ? rsb1 : rsb);                                     \
-    const int skt = more_here ? kt + 1 : 0;                                                        \
-    _Pragma("unroll") for (int p = 0; p < 4; ++p) {                                                \
-      if (p == 0 || p == 2) {                                                                      \
-        const int qm = p == 0 ? 0 : 1;                                                             \
-        _Pragma("unroll") for (int mi = 0; mi < 4; ++mi) {                                         \
-          const char* rr = ca + arow + (qm * 4 + mi) * 16 * 128;                                   \
-          af[mi][0] = *reinterpret_cast<const bf16x8*>(rr + ch0);                                  \
-          af[mi][1] = *reinterpret_cast<const bf16x8*>(rr + ch1);                                  \
-        }                                                                                          \
-      }                                                                                            \
-      if (p == 0 || p == 1) {                                                                      \
-        _Pragma("unroll") for (int ni = 0; ni < 2; ++ni) {                                         \
-          const char* rr = ca + brow + (p * 2 + ni) * 16 * 128;                                    \
-          const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(rr + ch0);                            \
-          const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(rr + ch1);                            \
-          if (p == 0) { b0[ni][0] = x0; b0[ni][1] = x1; } else { b1[ni][0] = x0; b1[ni][1] = x1; } \
-        }                                                                                          \
-      }                                                                                            \
-      if (p == 0) stage2<0>(so, sra, srb, na, nb, skt);                                            \
-      if (p == 1) stage2<1>(so, sra, srb, na, nb, skt);                                            \
-      if (p == 2) stage2<2>(so, sra, srb, na, nb, skt);                                            \
-      if (p == 3) stage2<3>(so, sra, srb, na, nb, skt);                                            \
-      if (first && p < 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WAIT_FIRST) : "memory");      \
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                                        \
-      bar();                                                                                       \
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
-      __builtin_amdgcn_sched_barrier(0);                                                           \
-      __builtin_amdgcn_s_setprio(1);                                                               \
-      const int qm = (p == 2 || p == 3) ? 1 : 0;                                                   \
-      _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                             \
-        _Pragma("unroll") for (int ni = 0; ni < 2; ++ni)                                           \
-          _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                       \
-            const bf16x8 bb = (p == 1 || p == 2) ? b1[ni][ks] : b0[ni][ks];                        \
-            const int nn = ((p == 1 || p == 2) ? 2 : 0) + ni;                                      \
-            acc[qm * 4 + mi][nn] = mfma16(bb, af[mi][ks], acc[qm * 4 + mi][nn]);                   \
-          }                                                                                        \
-      __builtin_amdgcn_s_setprio(0);                                                               \
-      bar();                                                                                       \
-    }                                                                                              \
-  } while (0)
-
-template <int EPI, bool DYN>
-__global__ void __launch_bounds__(512, 2) gemm_bt_persistent2(GemmArgs g) {
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
-  // the wave index through readfirstlane: provably uniform, so the LDS-DMA destinations (M0) are
-  // formed with scalar adds instead of a v_readfirstlane per DMA (-11 % VALU; +2-3 % vs hipBLASLt
-  // on the BERT projection shapes, profiles/r3_gemm_u2_experiment.jsonl)
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 15, lq = lane >> 4, sw = li & 7;
-  const int wm = w >> 2, wn = w & 3;
-  const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn;
-  const int nk = g.K / BK;
-  // tile sequence of this workgroup: XCD group x gets tiles [beg, end), member l takes beg + l + 32 i
-  const int nwg = gridDim.x, x = blockIdx.x % 8, l = blockIdx.x / 8, per = nwg / 8;
-  const int q = ntiles / 8, r = ntiles % 8;
-  const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-  const int end = beg + q + (x < r ? 1 : 0);
-  constexpr bool dyn = DYN;   // g.sched != null (a separate instantiation keeps SGPR pressure)
-  // dynamic queue: a workgroup's first two tiles are the static order's (no claims at launch,
-  // where 256 workgroups would contend for 8 counters); queue entry c is tile beg + 2 per + c.
-  // Iteration j >= 1 reads the tile of iteration j + 1 from qslot[j & 1].
-  __shared__ int qslot[2];
-  int t = beg + l;
-  if (t >= end) {   // more workgroups than tiles in this group (small problems) / queue drained
-    if constexpr (DYN) sched_finish(g.sched, nwg, tid);
-    return;
-  }
-  int m0, n0;
-  tile_of(t, ntn, m0, n0);
-  const StageOffs so = stage_offsets2(w, lane, g.lda, g.ldb);
-  auto rsa = uniform_rsrc(g.a + (size_t)m0 * g.lda), rsb = uniform_rsrc(g.b + (size_t)n0 * g.ldb);
-  stage2<0>(so, rsa, rsb, smem, smem + 2 * A_BYTES, 0);
-  stage2<1>(so, rsa, rsb, smem, smem + 2 * A_BYTES, 0);
-  stage2<2>(so, rsa, rsb, smem, smem + 2 * A_BYTES, 0);
-  stage2<3>(so, rsa, rsb, smem, smem + 2 * A_BYTES, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (__builtin_amdgcn_readfirstlane(wm) == 1) bar();   // stagger wave row 1
-
-  const int arow = (wm * 128 + li) * 128;
-  const int brow = 2 * A_BYTES + (wn * 64 + li) * 128;   // B halves at 64 KiB
-  const int ch0 = ((0 * 4 + lq) ^ sw) * 16, ch1 = ((1 * 4 + lq) ^ sw) * 16;
-  constexpr int S = kStores(EPI);
-  constexpr int WAIT_FIRST = 4 + S > 63 ? 63 : 4 + S;
-
-  bf16x8 af[4][2], b0[2][2], b1[2][2];
-  f32x4 acc[8][4];
-  int it = 0;
-  STAMP_ID(0);
-  while (true) {
-    STAMP(0, it);
-    const int tn = dyn && it > 0 ? __builtin_amdgcn_readfirstlane(qslot[it & 1]) : t + per;
-    const bool has_next = tn < end;
-    int m1 = 0, n1 = 0;
-    if (has_next) tile_of(tn, ntn, m1, n1);
-    const auto rsa1 = uniform_rsrc(g.a + (size_t)m1 * g.lda), rsb1 = uniform_rsrc(g.b + (size_t)n1 * g.ldb);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // K-steps in pairs: buffer 0 then 1, compile-time (nk is even: host check)
-    DTD_KSTEP2(0, true, 0);
-    DTD_KSTEP2(1, false, 1);
-    for (int kt2 = 2; kt2 < nk; kt2 += 2) {
-      DTD_KSTEP2(0, false, kt2);
-      DTD_KSTEP2(1, false, kt2 + 1);
-    }
-
-    STAMP(2, it);
-    // ---- epilogue through the free LDS buffer (the last K-step's; the other one holds the
-    //      next tile's K-step 0), in two rounds of 128 rows: the wave row r writes its
-    //      accumulators (fp32 bias / residual, one bf16 rounding) as a [128][512 B] image
-    //      (8-byte slots XOR-swizzled by row & 15), then all 8 waves store 16 rows each as
-    //      512-byte row segments of 16-byte vectors.
-    // accumulators -> packed bf16 first (fp32 bias / residual, one rounding): halves the live
-    // registers for the rest of the epilogue
-    bf16x4 pk[8][4];
-    if constexpr (EPI == EPI_ADD) {
-      const auto rs = uniform_rsrc(g.c + (size_t)(m0 + wm * 128) * g.ldc + n0 + wn * 64);
-      const int voff = (li * g.ldc + 4 * lq) * 2;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        bf16x4 cin[4][4];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            cin[mi][ni] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(
-                                                         rs, voff + ni * 32, (h * 4 + mi) * 16 * g.ldc * 2, 0));
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              pk[h * 4 + mi][ni][k] = (bf16)(acc[h * 4 + mi][ni][k] + (float)cin[mi][ni][k]);
-      }
-    } else {
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (EPI == EPI_STORE || is_gelu_fwd(EPI)) {
-          if (g.bias) {
-            const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n0 + wn * 64 + ni * 16 + 4 * lq);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) bv[k] = (float)b4[k];
-          }
-        }
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) pk[mi][ni][k] = (bf16)(acc[mi][ni][k] + bv[k]);
-      }
-    }
-    if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
-    bar();                                                // every wave is done with `img`
-    // the image in the last K-step's buffer (1): rows 0-63 in its A half, 64-127 in its B half
-    char* const imgA = smem + A_BYTES;
-    char* const imgB = smem + 3 * A_BYTES - 64 * 512;
-    const int c = lane & 31;
-    // row-phase inputs first (GELU_BWD: U), so no later load wait holds back a store
-    bf16x8 uin[2][8];
-    if constexpr (is_gelu_bwd(EPI)) {
-      const auto rs = uniform_rsrc(g.u + (size_t)m0 * g.ldu + n0);
-      const int voff = ((w * 16 + (lane >> 5)) * g.ldu + c * 8) * 2;
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          uin[rr][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      rs, voff, (rr * 128 + 2 * i) * g.ldu * 2, 0));
-    }
-    float colsum[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
-    int claim = 0;
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      // dynamic queue: claim the tile after the next one when the second round starts (every load
-      // of the epilogue is older, so no counted wait for them waits for the atomic as well);
-      // publish it when the round ends
-      if (dyn && rr == 1 && has_next && tid == 0) claim = atomicAdd(&g.sched[x], 1);
-      if (__builtin_amdgcn_readfirstlane(wm) == rr) {
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const int n = wn * 64 + ni * 16 + 4 * lq;
-#pragma unroll
-          for (int mi = 0; mi < 8; ++mi) {
-            const int m = mi * 16 + li;   // row within the round's 128
-            *reinterpret_cast<bf16x4*>((mi < 4 ? imgA : imgB) + m * 512 + (((n >> 2) ^ (m & 15)) << 3)) = pk[mi][ni];
-          }
-        }
-      }
-      bar();
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = w * 16 + 2 * i + (lane >> 5);   // row within the round
-        const int x = r & 15;
-        bf16x8 v = *reinterpret_cast<const bf16x8*>((w < 4 ? imgA : imgB) + r * 512 + ((c ^ (x >> 1)) << 4));
-        if (x & 1) v = __builtin_shufflevector(v, v, 4, 5, 6, 7, 0, 1, 2, 3);
-        const size_t off = (size_t)(m0 + rr * 128 + r) * g.ldc + n0 + c * 8;
-        if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
-          *reinterpret_cast<bf16x8*>(g.c + off) = v;
-        } else if constexpr (stores_grad(EPI)) {
-          bf16x8 av, dv;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float aj, dj;
-            epi_act_and_grad<EPI>((float)v[j], aj, dj);
-            av[j] = (bf16)aj;
-            dv[j] = (bf16)dj;
-          }
-          *reinterpret_cast<bf16x8*>(g.c + off) = dv;
-          *reinterpret_cast<bf16x8*>(g.c2 + off) = av;
-        } else if constexpr (is_gelu_fwd(EPI)) {
-          bf16x8 av;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) av[j] = (bf16)epi_act<EPI>((float)v[j]);
-          *reinterpret_cast<bf16x8*>(g.c + off) = v;
-          *reinterpret_cast<bf16x8*>(g.c2 + off) = av;
-        } else {
-          bf16x8 o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float du = (float)v[j] * epi_act_grad<EPI>((float)uin[rr][i][j]);
-            o[j] = (bf16)du;
-            colsum[j] += du;
-          }
-          *reinterpret_cast<bf16x8*>(g.c + off) = o;
-        }
-      }
-      if (dyn && rr == 1 && tid == 0) qslot[(it + 1) & 1] = has_next ? beg + 2 * per + claim : end;
-      bar();   // the image is consumed before it is rewritten / restaged
-    }
-    if constexpr (is_gelu_bwd(EPI)) {
-      // lanes c and c+32 hold the same columns; the 8 waves combine through LDS: one fp32
-      // partial row per 256-row tile
-#pragma unroll
-      for (int j = 0; j < 8; ++j) colsum[j] += __shfl_xor(colsum[j], 32, 64);
-      float* red = reinterpret_cast<float*>(imgA);
-      if (lane < 32) {
-        *reinterpret_cast<f32x4*>(red + w * 256 + c * 8) = f32x4{colsum[0], colsum[1], colsum[2], colsum[3]};
-        *reinterpret_cast<f32x4*>(red + w * 256 + c * 8 + 4) = f32x4{colsum[4], colsum[5], colsum[6], colsum[7]};
-      }
-      bar();
-      if (tid < 256 && g.part) {
-        float sum = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sum += red[k * 256 + tid];
-        g.part[(size_t)(m0 >> 8) * g.N + n0 + tid] = sum;
-      }
-      bar();
-    }
-    if (has_next && __builtin_amdgcn_readfirstlane(wm) == 1) bar();   // reopen the stagger
-    STAMP(4, it);
-    ++it;
-    if (!has_next) break;
-    t = tn;
-    m0 = m1;
-    n0 = n1;
-    rsa = rsa1;
-    rsb = rsb1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last K-step's duplicate stage
-  if constexpr (DYN) sched_finish(g.sched, nwg, tid);
-}
-
-#undef DTD_KSTEP2
 
 // W [rows][cols] -> WT [cols][rows], bf16, 64 x 64 tiles through LDS (padded rows).  Vector form
 // (rows, cols multiples of 8): 16-byte global loads and stores; otherwise element-wise.
@@ -1373,11 +1064,8 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
     const int cus = num_cus() / 8 * 8;
     const int nwg = ntiles >= cus ? cus : (ntiles + 7) / 8 * 8;
     g.sched = sched;
-    const bool split = gemm_variant() >= 2 && (K / BK) % 2 == 0;
-#define DTD_GEMM_P(E)                                                                                 \
-  if (split && sched) hipLaunchKernelGGL((gemm_bt_persistent2<E, true>), dim3(nwg), dim3(512), 0, s, g);     \
-  else if (split) hipLaunchKernelGGL((gemm_bt_persistent2<E, false>), dim3(nwg), dim3(512), 0, s, g);        \
-  else if (sched) hipLaunchKernelGGL((gemm_bt_persistent<E, true>), dim3(nwg), dim3(512), 0, s, g);          \
+#define DTD_GEMM_P(E)                                                                       \
+  if (sched) hipLaunchKernelGGL((gemm_bt_persistent<E, true>), dim3(nwg), dim3(512), 0, s, g);   \
   else hipLaunchKernelGGL((gemm_bt_persistent<E, false>), dim3(nwg), dim3(512), 0, s, g)
     switch (epi) {
       case EPI_STORE: DTD_GEMM_P(EPI_STORE); break;
