@@ -22,6 +22,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..ops import functional as Fx
+from ..ops import gemm as G
 from ..ops.grad import emit_wgrad, grad_done, grad_dst, note_use
 
 from .config import TransformerConfig
@@ -233,7 +234,7 @@ class _MLMHeadFn(torch.autograd.Function):
             del logits
         grad_done(head.decoder_bias)
         emit_wgrad(head.decoder_weight, dlogits, t)
-        dt = dlogits @ head.decoder_weight
+        dt = G.dgrad(dlogits, head.decoder_weight)
         da, _ = Fx.ln_bwd(dt, None, a, m, r, head.ln_g, 0.0, ctx.rng, 0, want_dz=True,
                           dgamma=grad_dst(head.ln_g), dbeta=grad_dst(head.ln_b))
         grad_done(head.ln_g)
@@ -241,7 +242,7 @@ class _MLMHeadFn(torch.autograd.Function):
         du = Fx.act_bwd(da, u, c.activation, dbias=grad_dst(head.dense_b))
         grad_done(head.dense_b)
         emit_wgrad(head.dense_w, du, x)
-        dx = du @ head.dense_w
+        dx = G.dgrad(du, head.dense_w)
         return (dx, None, None) + (None,) * len(head.params())
 
 

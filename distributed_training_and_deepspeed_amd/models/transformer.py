@@ -208,6 +208,10 @@ _FUSED_QKV_BIAS = [os.environ.get("DTD_ATTN_QKV_BIAS", "1") == "1"]
 _LN_MEMEFF = [os.environ.get("DTD_LN_MEMEFF", "1") == "1"]
 
 
+_wt = G.transposed_for_dgrad
+_dgrad = G.dgrad
+
+
 def _acc(p):
     return grad_dst(p)
 
@@ -328,7 +332,7 @@ class _FusedLayerFn(torch.autograd.Function):
             du = G.gelu_bwd_gemm(dy, w2t, u, dbias=_acc(bf1), act=c.activation)
             del w2t
         else:
-            da = dy @ w2
+            da = _dgrad(dy, w2)
             if a is None:
                 du, a = Fx.act_bwd(da, u, c.activation, dbias=_acc(bf1), want_act=True)
             else:
@@ -338,7 +342,7 @@ class _FusedLayerFn(torch.autograd.Function):
         del a
         emit_wgrad(w1, du, f_in, async_ok=True)
         if c.pre_ln:
-            dfin = du @ w1
+            dfin = _dgrad(du, w1)
             # z1 = x + dropout(o); f_in = LN2(z1); dz1 also receives dout (residual of out)
             dz1, do = Fx.ln_bwd(dfin, dout, z1, m2, r2, g2, p_h, rng, s1, want_dz=True, want_dy=True,
                                 dgamma=_acc(g2), dbeta=_acc(b2), dbias=_acc(o_b))
@@ -347,14 +351,14 @@ class _FusedLayerFn(torch.autograd.Function):
         else:
             # f_in = LN1(z1) feeds both the FFN and (as residual) z2: d f_in = du.W1 + dz2, with
             # the residual term summed inside the LN kernel (no addmm C-copy, no add pass)
-            dfin = du @ w1
+            dfin = _dgrad(du, w1)
             lo1 = dict(xout=f_in, beta=b1) if ctx.ln_fo else {}
             dz1, do = Fx.ln_bwd(dfin, None, z1, m1, r1, g1, p_h, rng, s1, want_dz=True, want_dy=True,
                                 dgamma=_acc(g1), dbeta=_acc(b1), dbias=_acc(o_b), dout2=dz2, **lo1)
             for p in (g1, b1, o_b):
                 grad_done(p)
         emit_wgrad(o_w, do, actx, async_ok=True)
-        dctx = do @ o_w
+        dctx = _dgrad(do, o_w)
         # the qkv bias gradient comes out of the attention-backward epilogues (column partials)
         if _FUSED_QKV_BIAS[0]:
             dqkv = A.attn_bwd(dctx, qkv, actx, lse, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, ctx.amask,
@@ -365,14 +369,16 @@ class _FusedLayerFn(torch.autograd.Function):
         grad_done(qkv_b)
         if c.pre_ln:
             emit_wgrad(qkv_w, dqkv, a_in, async_ok=True)
-            dain = dqkv @ qkv_w
+            dain = _dgrad(dqkv, qkv_w)
             dx, _ = Fx.ln_bwd(dain, dz1, x2d, m1, r1, g1, 0.0, rng, 0, want_dz=True, want_dy=False,
                               dgamma=_acc(g1), dbeta=_acc(b1))
             for p in (g1, b1):
                 grad_done(p)
         else:
             emit_wgrad(qkv_w, dqkv, x2d, async_ok=True)
-            dx = dz1.addmm_(dqkv, qkv_w)   # in place: dz1 is this backward's own buffer (no C copy)
+            qkv_wt = _wt(qkv_w)
+            # in place: dz1 is this backward's own buffer (no C copy); NT form through the transposed view
+            dx = dz1.addmm_(dqkv, qkv_w if qkv_wt is None else qkv_wt.t())
         return (dx.view(B, S, h), None) + (None,) * 12
 
 

@@ -214,6 +214,30 @@ def transpose(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# Input-gradient products as "NT" GEMMs (DTD_DGRAD_NT=0: dy @ W): dX = dY W computed as
+# F.linear(dY, W^T) with W^T materialised by `transpose` (~1-4 us a BERT-base weight), so hipBLASLt
+# runs its forward-layout kernels instead of the NN ones -- at BERT-base b256 the qkv / o / fc1
+# input gradients take 322-335 / 126-135 / 428-441 us that way vs 390 / 159-166 / 501-508 us
+# (profiles/r3_gemm_split_experiment.jsonl: bench_gemm8's "dgrad_*" hipBLASLt column vs
+# bench_gemm_v2's, same session).
+_DGRAD_NT = [os.environ.get("DTD_DGRAD_NT", "1") == "1"]
+
+
+def transposed_for_dgrad(w: torch.Tensor) -> torch.Tensor | None:
+    """W^T contiguous for the NT input-gradient form, or None (keep dy @ W)."""
+    if not (_DGRAD_NT[0] and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()):
+        return None
+    if w.shape[0] % 8:   # W^T rows (the GEMM's K) would not be 16-byte aligned (e.g. a 28996-row vocabulary)
+        return None
+    return transpose(w)
+
+
+def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dy @ w for a Linear weight w [out, in], through the NT form when it applies."""
+    wt = transposed_for_dgrad(w)
+    return dy @ w if wt is None else torch.nn.functional.linear(dy, wt)
+
+
 def wgrad_preferred(o: int, i: int) -> bool:
     """Where the TN kernel beats hipBLASLt's split-K bmm: small weights (<= 16 output tiles of
     256 x 256, e.g. the 768 x 768 attention output projection: 165 vs 176 us at 131k tokens).  Its
