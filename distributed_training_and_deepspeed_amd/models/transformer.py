@@ -208,7 +208,6 @@ _FUSED_QKV_BIAS = [os.environ.get("DTD_ATTN_QKV_BIAS", "1") == "1"]
 _LN_MEMEFF = [os.environ.get("DTD_LN_MEMEFF", "1") == "1"]
 
 
-_wt = G.transposed_for_dgrad
 _dgrad = G.dgrad
 
 
@@ -251,9 +250,9 @@ class _FusedLayerFn(torch.autograd.Function):
             _, a_in, m1, r1 = Fx.ln_fwd(None, x2d, g1, b1, eps, 0.0, rng, 0)
         else:
             a_in = x2d
-        qkv = F.linear(a_in, qkv_w, qkv_b)
+        qkv = G.linear_any(a_in, qkv_w, qkv_b)
         actx, lse, amask = A.attn_fwd(qkv, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, masks=pend)
-        o = F.linear(actx, o_w, o_b)
+        o = G.linear_any(actx, o_w, o_b)
         ln_fo = _LN_MEMEFF[0] and not c.pre_ln
         if c.pre_ln:
             z1, f_in, m2, r2 = Fx.ln_fwd(o, x2d, g2, b2, eps, p_h, rng, s1)
@@ -269,9 +268,9 @@ class _FusedLayerFn(torch.autograd.Function):
             else:
                 u, a = G.linear_gelu(f_in, w1, bf1, c.activation)     # fc1 + bias + GELU in one kernel
         else:
-            u = F.linear(f_in, w1, bf1)
+            u = G.linear_any(f_in, w1, bf1)
             a = Fx.act_fwd(u, c.activation)
-        y = F.linear(a, w2, bf2)
+        y = G.linear_any(a, w2, bf2)
         if c.pre_ln:
             out = Fx.dropout_add(y, z1, p_h, rng, s2)
             z2 = m3 = r3 = None
@@ -376,9 +375,8 @@ class _FusedLayerFn(torch.autograd.Function):
                 grad_done(p)
         else:
             emit_wgrad(qkv_w, dqkv, x2d, async_ok=True)
-            qkv_wt = _wt(qkv_w)
-            # in place: dz1 is this backward's own buffer (no C copy); NT form through the transposed view
-            dx = dz1.addmm_(dqkv, qkv_w if qkv_wt is None else qkv_wt.t())
+            # in place: dz1 is this backward's own buffer (no C copy); NT form through the transposed weight
+            dx = G.dgrad_add_(dz1, dqkv, qkv_w)
         return (dx.view(B, S, h), None) + (None,) * 12
 
 

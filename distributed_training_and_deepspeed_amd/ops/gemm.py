@@ -60,6 +60,12 @@ _FFN_STORE_GRAD = [os.environ.get("DTD_GEMM_FFN_STORE_GRAD", "1") == "1"]
 # (profiles/r2_ab_gemm_oproj.jsonl).  The NT kernel on the transposed o-projection weight (152 vs
 # 164 us in isolation) was neutral end-to-end as well and is not wired in.
 _WGRAD = [os.environ.get("DTD_GEMM_WGRAD", "0") == "1"]
+# DTD_GEMM_ALL=1: every transformer-layer projection on the hand-written kernels -- forward
+# (gemm_bt + bias), input gradients (gemm_bt on the transposed weight), weight gradients (TN
+# kernel, fp32 split-K partials) -- no vendor GEMM in the layers.  Off by default: the NT main loop
+# runs at 0.86-0.92x of hipBLASLt's kernels on the plain products
+# (profiles/r3_gemm_u2_experiment.jsonl); kept as the fully native compute path and for A/B runs.
+_ALL = [os.environ.get("DTD_GEMM_ALL", "0") == "1"]
 # Tile order of the persistent kernel: "dynamic" (default) claims tiles from a per-stream atomic
 # queue, so workgroups delayed by CUs that another stream holds (RCCL on the comm stream, the
 # attention-mask generator) take fewer tiles; "static" is the fixed round-robin order (A/B runs).
@@ -87,7 +93,23 @@ def ffn_store_grad_enabled() -> bool:
 
 
 def wgrad_enabled() -> bool:
-    return _ENABLED[0] and _WGRAD[0]
+    return _ENABLED[0] and (_WGRAD[0] or _ALL[0])
+
+
+def all_enabled() -> bool:
+    return _ENABLED[0] and _ALL[0]
+
+
+def set_all(on: bool) -> None:
+    _ALL[0] = bool(on)
+
+
+def linear_any(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    """F.linear, or the hand-written kernel in the all-native mode when the shape tiles."""
+    if all_enabled() and x.dim() == 2 and supported(x.shape[0], w.shape[0], x.shape[1], x, w) and (
+            b is None or (b.is_cuda and b.dtype == torch.bfloat16 and b.is_contiguous())):
+        return linear(x, w, b)
+    return torch.nn.functional.linear(x, w, b)
 
 
 def set_enabled(on: bool) -> None:
@@ -233,17 +255,33 @@ def transposed_for_dgrad(w: torch.Tensor) -> torch.Tensor | None:
 
 
 def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """dy @ w for a Linear weight w [out, in], through the NT form when it applies."""
+    """dy @ w for a Linear weight w [out, in], through the NT form when it applies (the
+    hand-written kernel in the all-native mode)."""
     wt = transposed_for_dgrad(w)
-    return dy @ w if wt is None else torch.nn.functional.linear(dy, wt)
+    if wt is None:
+        return dy @ w
+    if all_enabled() and dy.dim() == 2 and supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt):
+        return matmul_nt(dy, wt)
+    return torch.nn.functional.linear(dy, wt)
+
+
+def dgrad_add_(c: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """c += dy @ w in place (residual-branch input gradient), NT form when it applies."""
+    wt = transposed_for_dgrad(w)
+    if wt is None:
+        return c.addmm_(dy, w)
+    if all_enabled() and dy.dim() == 2 and supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c):
+        return matmul_nt_add_(c, dy, wt)
+    return c.addmm_(dy, wt.t())
 
 
 def wgrad_preferred(o: int, i: int) -> bool:
     """Where the TN kernel beats hipBLASLt's split-K bmm: small weights (<= 16 output tiles of
     256 x 256, e.g. the 768 x 768 attention output projection: 165 vs 176 us at 131k tokens).  Its
     transposing-read main loop runs ~0.85 PF/s, below hipBLASLt on the larger weights
-    (profiles/r2_gemm8_vs_hipblaslt.jsonl), so those stay on the library."""
-    return (o // 256) * (i // 256) <= 16
+    (profiles/r2_gemm8_vs_hipblaslt.jsonl), so those stay on the library (all of them take the
+    kernel in the all-native mode)."""
+    return _ALL[0] or (o // 256) * (i // 256) <= 16
 
 
 def wgrad_supported(dy: torch.Tensor, x: torch.Tensor) -> bool:

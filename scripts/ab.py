@@ -79,7 +79,7 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "attn_occ_322": _env(DTD_ATTN_OCC="3,2,2"), "attn_occ_323_dq64": _env(DTD_ATTN_OCC="3,2,3", DTD_ATTN_TILE="64,64"),
            "wgrad_s1": _wgrad_fixed(1), "wgrad_s4": _wgrad_fixed(4), "wgrad_s8": _wgrad_fixed(8),
            "gemm_split": _env(DTD_GEMM_VARIANT="2"), "dgrad_nn": _env(DTD_DGRAD_NT="0"),
-           "dkdv_bm64": _env(DTD_ATTN_DKDV_BM="64"),
+           "dkdv_bm64": _env(DTD_ATTN_DKDV_BM="64"), "gemm_all": _env(DTD_GEMM_ALL="1"),
            "attn_fwd_pipe": _env(DTD_ATTN_FWD="pipe"), "attn_pk": _env(DTD_ATTN_FWD_PK="1"),
            "ln_memeff_off": _env(DTD_LN_MEMEFF="0"), "ln_bwd_prefetch": _env(DTD_LN_BWD_PREFETCH="1"),
            "base": lambda: None, "old_wgrad_split": _old_wgrad_split, "f32_wgrad_partials": _f32_wgrad_partials,
