@@ -38,6 +38,8 @@
 // 256 x 256 bf16 image (8-byte column slots XOR-swizzled by row & 15: conflict-free writes), and
 // are read back row-major so every global store (and the GELU-backward U load) is a full 512-byte
 // row segment of 16-byte vectors.  XCD-aware bijective tile order (T1).
+#include <type_traits>
+
 #include "common.h"
 
 using namespace dtd;
@@ -180,6 +182,15 @@ __device__ __forceinline__ void epi_act_and_grad(float x, float& a, float& d) {
 __device__ __forceinline__ float gelu_grad(float x) {
   const float e = gauss_e(x);
   return fmaf(x * 0.3989422804014327f, e, phi_cdf(x, e));
+}
+
+// fp32 x 4 -> bf16 x 4 as two v_cvt_pk_bf16_f32 (element-wise casts of a vector make hipcc convert
+// one element per instruction and re-pack with v_perm / v_alignbit)
+__device__ __forceinline__ bf16x4 cvt4(f32x4 v) {
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2 lo = __builtin_convertvector(f32x2_t{v[0], v[1]}, bf16x2);
+  const bf16x2 hi = __builtin_convertvector(f32x2_t{v[2], v[3]}, bf16x2);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3);
 }
 
 // bijective XCD remap of the linear workgroup id (dispatch deals ids round-robin over 8 XCDs):
@@ -727,12 +738,10 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
     int m1 = 0, n1 = 0;
     if (has_next) tile_of(tn, ntn, m1, n1);
     const auto rsa1 = uniform_rsrc(g.a + (size_t)m1 * g.lda), rsb1 = uniform_rsrc(g.b + (size_t)n1 * g.ldb);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int kt = 0; kt < nk; ++kt) {
+    // K-step 0 is peeled: its first MFMA per accumulator takes an inline-zero C operand, so the
+    // 128 accumulators need no v_mov zeroing per tile (the MFMA pipe idles during that block)
+    auto kstep = [&](auto first_c, int kt) {
+      constexpr bool first = decltype(first_c)::value;
       const char* cur = smem + buf * TILE_BYTES;
       char* nxt = smem + (buf ^ 1) * TILE_BYTES;
       buf ^= 1;
@@ -742,7 +751,6 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
       const bool more = more_here || has_next;
       const auto sra = more_here ? rsa : rsa1, srb = more_here ? rsb : rsb1;
       const int skt = more_here ? kt + 1 : 0;
-      const bool first = kt == 0;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         if (p == 0 || p == 2) {
@@ -789,12 +797,15 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
             for (int ks = 0; ks < 2; ++ks) {
               const bf16x8 bb = (p == 1 || p == 2) ? b1[ni][ks] : b0[ni][ks];
               const int nn = ((p == 1 || p == 2) ? 2 : 0) + ni;
-              acc[qm * 4 + mi][nn] = mfma16(bb, af[mi][ks], acc[qm * 4 + mi][nn]);
+              acc[qm * 4 + mi][nn] =
+                  mfma16(bb, af[mi][ks], (first && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[qm * 4 + mi][nn]);
             }
         __builtin_amdgcn_s_setprio(0);
         bar();
       }
-    }
+    };
+    kstep(std::true_type{}, 0);
+    for (int kt = 1; kt < nk; ++kt) kstep(std::false_type{}, kt);
 
     STAMP(2, it);
     // ---- epilogue through the free LDS buffer (the last K-step's; the other one holds the
@@ -821,9 +832,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
           for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              pk[h * 4 + mi][ni][k] = (bf16)(acc[h * 4 + mi][ni][k] + (float)cin[mi][ni][k]);
+            pk[h * 4 + mi][ni] = cvt4(acc[h * 4 + mi][ni] + __builtin_convertvector(cin[mi][ni], f32x4));
       }
     } else {
 #pragma unroll
@@ -836,10 +845,9 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
             for (int k = 0; k < 4; ++k) bv[k] = (float)b4[k];
           }
         }
+        const f32x4 bv4{bv[0], bv[1], bv[2], bv[3]};
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) pk[mi][ni][k] = (bf16)(acc[mi][ni][k] + bv[k]);
+        for (int mi = 0; mi < 8; ++mi) pk[mi][ni] = cvt4(acc[mi][ni] + bv4);
       }
     }
     if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
@@ -875,7 +883,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
 #pragma unroll
           for (int mi = 0; mi < 8; ++mi) {
             const int m = mi * 16 + li;   // row within the round's 128
-            *reinterpret_cast<bf16x4*>(img + m * 512 + (((n >> 2) ^ (m & 15)) << 3)) = pk[mi][ni];
+            *reinterpret_cast<bf16x4*>(img + m * 512 + (((n >> 2) ^ ((m & 15) << 1)) << 3)) = pk[mi][ni];
           }
         }
       }
@@ -883,9 +891,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int r = w * 16 + 2 * i + (lane >> 5);   // row within the round
-        const int x = r & 15;
-        bf16x8 v = *reinterpret_cast<const bf16x8*>(img + r * 512 + ((c ^ (x >> 1)) << 4));
-        if (x & 1) v = __builtin_shufflevector(v, v, 4, 5, 6, 7, 0, 1, 2, 3);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + r * 512 + ((c ^ (r & 15)) << 4));
         const size_t off = (size_t)(m0 + rr * 128 + r) * g.ldc + n0 + c * 8;
         if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
           *reinterpret_cast<bf16x8*>(g.c + off) = v;

@@ -160,24 +160,30 @@ def test_all_native_gemm_mode_matches_library_gemms(monkeypatch):
     from distributed_training_and_deepspeed_amd.ops import gemm as G
     from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
     calls = {"bt": 0, "tn": 0}
-    bt, tn = G.gemm_bt, G.wgrad_tn
+    bt, tn, add = G.gemm_bt, G.wgrad_tn, G.matmul_nt_add_
 
     def count_bt(*a, **k):
         calls["bt"] += 1
         return bt(*a, **k)
+
+    def count_add(*a, **k):
+        calls["bt"] += 1
+        return add(*a, **k)
 
     def count_tn(*a, **k):
         calls["tn"] += 1
         return tn(*a, **k)
     monkeypatch.setattr(G, "gemm_bt", count_bt)
     monkeypatch.setattr(G, "wgrad_tn", count_tn)
+    monkeypatch.setattr(G, "matmul_nt_add_", count_add)
     out = []
     for on in (False, True):
         G.set_all(on)
         try:
             model = build_model("bert-base-cased", dtype=torch.bfloat16, device="cuda", seed=11)
             ddp = DistributedDataParallel(model)
-            ds = SyntheticLMDataset(model.cfg, 4, seq_len=512, seed=2)
+            # 16 x 512 = 8192 tokens: the smallest token count the weight-gradient TN path takes
+            ds = SyntheticLMDataset(model.cfg, 16, seq_len=512, seed=2)
             loss = ddp(ds.input_ids.cuda(), labels=ds.labels.cuda()).loss
             loss.backward()
             torch.cuda.synchronize()
@@ -187,9 +193,9 @@ def test_all_native_gemm_mode_matches_library_gemms(monkeypatch):
         if not on:
             base = dict(calls)
     L = model.cfg.num_layers
-    # per layer: 3 forward projections (fc1 is the fused GEMM+GELU kernel in both modes) and 3
-    # input gradients through gemm_bt (the 4th, the residual qkv one, is the in-place EPI_ADD
-    # form), 4 weight gradients through the TN kernel
+    # per layer: 3 forward projections (fc1 is the fused GEMM+GELU kernel in both modes), 2 input
+    # gradients through gemm_bt and the residual qkv one in the in-place EPI_ADD form (fc2's is
+    # the fused GELU-backward kernel in both modes), 4 weight gradients through the TN kernel
     assert calls["bt"] - base["bt"] >= 6 * L, (base, calls)
     assert calls["tn"] - base["tn"] >= 4 * L, (base, calls)
     assert abs(out[0][0] - out[1][0]) <= 1e-2 * abs(out[0][0])
