@@ -40,6 +40,10 @@
 // row segment of 16-byte vectors.  XCD-aware bijective tile order (T1).
 #include <type_traits>
 
+#ifndef DTD_GEMM_DIAG
+#define DTD_GEMM_DIAG 0
+#endif
+
 #include "common.h"
 
 using namespace dtd;
@@ -753,6 +757,9 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
       const int skt = more_here ? kt + 1 : 0;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
+#if DTD_GEMM_DIAG & 2   // diagnostic build: fragments read in the first K-step only
+        if (first)
+#endif
         if (p == 0 || p == 2) {
           const int qm = p == 0 ? 0 : 1;
 #pragma unroll
@@ -762,6 +769,9 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
             af[mi][1] = *reinterpret_cast<const bf16x8*>(rr + ch1);
           }
         }
+#if DTD_GEMM_DIAG & 2
+        if (first)
+#endif
         if (p == 0 || p == 1) {
 #pragma unroll
           for (int ni = 0; ni < 2; ++ni) {
@@ -772,10 +782,16 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
           }
         }
         if (more) {
+#if DTD_GEMM_DIAG & 1   // diagnostic build (timing only, wrong results): no main-loop LDS-DMA
+          if (first) {
+#endif
           if (p == 0) stage<0>(so, sra, srb, nxt, skt);
           if (p == 1) stage<1>(so, sra, srb, nxt, skt);
           if (p == 2) stage<2>(so, sra, srb, nxt, skt);
           if (p == 3) stage<3>(so, sra, srb, nxt, skt);
+#if DTD_GEMM_DIAG & 1
+          }
+#endif
           if (first && p < 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WAIT_FIRST) : "memory");
           else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         } else if (p == 0) {
@@ -784,7 +800,9 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+#if !(DTD_GEMM_DIAG & 4)   // diagnostic build: no barriers in the main loop
         bar();
+#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
@@ -801,7 +819,9 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
                   mfma16(bb, af[mi][ks], (first && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[qm * 4 + mi][nn]);
             }
         __builtin_amdgcn_s_setprio(0);
+#if !(DTD_GEMM_DIAG & 4)
         bar();
+#endif
       }
     };
     kstep(std::true_type{}, 0);

@@ -99,6 +99,13 @@ def main():
         "dgrad_fc2_mul_bwd": (2 * T * H * F, lambda: Fx.act_bwd(x @ w["fc2"], u, "gelu", dbias=(db, False)),
                               lambda: G.mul_bwd_gemm(x, wt["fc2"], u, dbias=(db, False))),
         "transpose_fc1": (0, lambda: None, lambda: G.transpose(w["fc1"])),
+        # input gradients as the model's default issues them: hipBLASLt in the NT form on the
+        # transposed weight (its forward-layout kernels), vs the same kernel as above
+        "dgradnt_qkv": (2 * T * H * 3 * H, lambda: L(dy3, wt["qkv"]), lambda: G.matmul_nt(dy3, wt["qkv"])),
+        "dgradnt_add_qkv": (2 * T * H * 3 * H, lambda: res.addmm_(dy3, wt["qkv"].t()),
+                            lambda: G.matmul_nt_add_(res, dy3, wt["qkv"])),
+        "dgradnt_o": (2 * T * H * H, lambda: L(x, wt["o"]), lambda: G.matmul_nt(x, wt["o"])),
+        "dgradnt_fc1": (2 * T * H * F, lambda: L(xf, wt["fc1"]), lambda: G.matmul_nt(xf, wt["fc1"])),
     }
     # weight gradients: hipBLASLt split-K (16 x T/16-token slices, bf16 partials) + reduce vs the
     # TN kernel (fp32 partials, one wave of workgroups) + reduce

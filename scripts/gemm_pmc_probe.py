@@ -30,12 +30,28 @@ def run():
     print("ok", flush=True)
 
 
+def run_wgrad():
+    """fc1 weight gradient (dW [3072, 768] = dU^T X over T = 131072 tokens): the TN kernel's fp32
+    split-K partials vs hipBLASLt's 16-slice bmm (the model's default), three launches each."""
+    from distributed_training_and_deepspeed_amd.ops import gemm as G
+    from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
+    use_tuned_gemms()
+    T, o, i = 131072, 3072, 768
+    dy = torch.rand(T, o, device="cuda", dtype=torch.bfloat16) * 2 - 1
+    x = torch.rand(T, i, device="cuda", dtype=torch.bfloat16) * 2 - 1
+    for _ in range(3):
+        G.wgrad_tn(dy, x)
+        torch.bmm(dy.view(16, T // 16, o).transpose(1, 2), x.view(16, T // 16, i))
+    torch.cuda.synchronize()
+    print("ok", flush=True)
+
+
 def summarize(paths):
     acc = defaultdict(lambda: defaultdict(list))
     for path in paths:
         for r in csv.DictReader(open(path)):
             name = r.get("Kernel_Name", "")
-            fam = "ours" if "gemm_bt" in name else ("hipblaslt" if "Cijk" in name else None)
+            fam = "ours" if ("gemm_bt" in name or "gemm_tn" in name) else ("hipblaslt" if "Cijk" in name else None)
             if fam is None:
                 continue
             grid = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
@@ -48,5 +64,7 @@ def summarize(paths):
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "summarize":
         summarize(sys.argv[2:])
+    elif len(sys.argv) > 1 and sys.argv[1] == "wgrad":
+        run_wgrad()
     else:
         run()
