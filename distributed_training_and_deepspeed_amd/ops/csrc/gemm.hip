@@ -43,6 +43,13 @@
 #ifndef DTD_GEMM_DIAG
 #define DTD_GEMM_DIAG 0
 #endif
+// DTD_GEMM_ONEBAR=1 (variant build): one barrier per phase and no wave-row stagger in the
+// persistent kernel -- both waves of a SIMD reach their MFMAs together and the matrix pipe
+// arbitrates between them (4 barriers per K-step instead of 8)
+#ifndef DTD_GEMM_ONEBAR
+#define DTD_GEMM_ONEBAR 0
+#endif
+constexpr bool kOneBar = DTD_GEMM_ONEBAR != 0;
 
 #include "common.h"
 
@@ -247,7 +254,14 @@ __device__ __forceinline__ StageOffs stage_offsets(int w, int lane, int lda, int
 template <int H>
 __device__ __forceinline__ void stage(const StageOffs& o, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb,
                                       char* buf, int kt) {
+#if DTD_GEMM_DIAG & 16   // diagnostic build: every K-step re-stages K-step 0 (L2-hot source)
+  const int so = 0 * kt;
+#else
   const int so = kt * BK * 2;
+#endif
+#if DTD_GEMM_DIAG & 32   // diagnostic build: only the A half-tiles are staged
+  if constexpr (H == 1 || H == 2) return;
+#endif
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     if constexpr (H == 0 || H == 3) {
@@ -722,7 +736,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
   stage<3>(so, rsa, rsb, smem, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (__builtin_amdgcn_readfirstlane(wm) == 1) bar();   // stagger wave row 1
+  if (!kOneBar && __builtin_amdgcn_readfirstlane(wm) == 1) bar();   // stagger wave row 1
 
   const int arow = (wm * 128 + li) * 128;
   const int brow = A_BYTES + (wn * 64 + li) * 128;
@@ -792,8 +806,10 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
 #if DTD_GEMM_DIAG & 1
           }
 #endif
+#if !(DTD_GEMM_DIAG & 8)   // diagnostic build: LDS-DMA issued but never waited for in the loop
           if (first && p < 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WAIT_FIRST) : "memory");
           else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#endif
         } else if (p == 0) {
           if (first) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WAIT_FIRST - 2) : "memory");
           else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -819,7 +835,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
                   mfma16(bb, af[mi][ks], (first && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[qm * 4 + mi][nn]);
             }
         __builtin_amdgcn_s_setprio(0);
-#if !(DTD_GEMM_DIAG & 4)
+#if !(DTD_GEMM_DIAG & 4) && !DTD_GEMM_ONEBAR
         bar();
 #endif
       }
@@ -870,7 +886,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
         for (int mi = 0; mi < 8; ++mi) pk[mi][ni] = cvt4(acc[mi][ni] + bv4);
       }
     }
-    if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
+    if (!kOneBar && __builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
     bar();                                                // every wave is done with `img`
     char* img = smem + (buf ^ 1) * TILE_BYTES;            // = the last K-step's buffer
     const int c = lane & 31;
@@ -965,7 +981,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
       }
       bar();
     }
-    if (has_next && __builtin_amdgcn_readfirstlane(wm) == 1) bar();   // reopen the stagger
+    if (!kOneBar && has_next && __builtin_amdgcn_readfirstlane(wm) == 1) bar();   // reopen the stagger
     STAMP(4, it);
     ++it;
     if (!has_next) break;

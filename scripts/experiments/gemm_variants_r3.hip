@@ -957,3 +957,36 @@ __global__ void __launch_bounds__(256, 1) gemm_bt_w4(GemmArgs g) {
 // 
 // #undef DTD_KSTEP2
 // 
+
+
+// ---------------------------------------------------------------------------------------------
+// Round 3b: register-staged B panel in gemm_bt_persistent (was DTD_GEMM_REGB=1).  After the
+// limiter probe (profiles/r3_gemm_limiter_probe.jsonl: LDS-DMA issue is the main-loop limiter,
+// ~90 cycles per buffer_load...lds among the phase's ds_reads; halving the DMA count recovers most
+// of the gap to the no-staging ceiling), the B half-tiles went through registers: global loads at
+// phases 1 / 2 into 2 x 16 B per lane, ds_write_b128 one phase later to the DMA's lane-linear image.
+// 252 VGPRs, no spill, tests/test_gemm_gpu.py 39 passed -- and 0.70x the DMA form (qkv 622 vs 443 us,
+// fc2 758 vs 471 us): the phase-2 / phase-3 waits retire loads issued one phase earlier, which the
+// L2 round trip does not meet (a two-phase register ring needs 16 more VGPRs: spills).  Removed.
+//   main loop (non-first K-steps, `more`):
+//     p0: stage<0>(A lo DMA);            vmcnt(4)
+//     p1: load_b<0>(B lo -> regs);       vmcnt(4)
+//     p2: vmcnt(0); store_b<0>(regs -> LDS); load_b<1>(B hi -> regs)
+//     p3: stage<3>(A hi DMA); vmcnt(2);  store_b<1>(regs -> LDS)
+// // Register-staged form of stage<1> / stage<2> (B rows lo / hi half): the same per-lane source
+// // (swizzled chunk) and the same lane-linear LDS destination as the LDS-DMA, as a global load into
+// // two 16-byte registers and, one phase later, two ds_write_b128.  An LDS-DMA instruction costs the
+// // issuing wave ~90 cycles among the phase's LDS reads (profiles/r3_gemm_limiter_probe.jsonl); the
+// // load + store pair a fraction of that.
+// template <int HB>
+// __device__ __forceinline__ void load_b(const StageOffs& o, __amdgpu_buffer_rsrc_t rb, int kt, bf16x8 (&r)[2]) {
+//   const int so = kt * BK * 2;
+// #pragma unroll
+//   for (int i = 0; i < 2; ++i)
+//     r[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, o.b[HB][i], so, 0));
+// }
+// template <int HB>
+// __device__ __forceinline__ void store_b(const StageOffs& o, char* buf, int lane, const bf16x8 (&r)[2]) {
+// #pragma unroll
+//   for (int i = 0; i < 2; ++i) *reinterpret_cast<bf16x8*>(buf + o.lb[HB][i] + lane * 16) = r[i];
+// }
