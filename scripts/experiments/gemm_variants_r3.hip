@@ -990,3 +990,11 @@ __global__ void __launch_bounds__(256, 1) gemm_bt_w4(GemmArgs g) {
 // #pragma unroll
 //   for (int i = 0; i < 2; ++i) *reinterpret_cast<bf16x8*>(buf + o.lb[HB][i] + lane * 16) = r[i];
 // }
+
+// ---------------------------------------------------------------------------------------------
+// Round 3b: LDS-DMA placement / priority in the persistent main loop (scripts/gemm_diag.py, same
+// box, 2 rounds; GEMM tests pass under each): DMA issued BEFORE the phase's fragment reads 0.63x
+// (the reads queue behind the DMA's LDS writes and the MFMA segment waits on them); DMA in the
+// middle of the MFMA segment 0.78x; no s_setprio around the MFMA segments 0.90x; both 0.75x; one
+// barrier per phase without the wave-row stagger 0.95x.  The shipped order (reads, then DMA, then
+// the counted wait and barrier; MFMA segment at priority 1) is the best of the set.
