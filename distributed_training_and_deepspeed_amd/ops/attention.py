@@ -117,6 +117,35 @@ def _side_stream(device) -> torch.cuda.Stream:
     return s
 
 
+def mask_words(B: int, H: int, S: int) -> int:
+    """Words per keep-bit layout of one attention call: [B*H][W][32 W], W = ceil(S / 32)."""
+    W = (S + 31) // 32
+    return B * H * W * 32 * W
+
+
+def _lm_pos(n: int) -> torch.Tensor:
+    """Word position of each of n positions inside its [32 W] row (ops/csrc/attention.hip lm_pos:
+    within a 32-group, c = 8a + 4b + j sits at 8a + 2j + b)."""
+    x = torch.arange(n)
+    c = x & 31
+    return (x & ~31) | (c & 24) | ((c & 3) << 1) | ((c >> 2) & 1)
+
+
+def decode_masks(masks: torch.Tensor, B: int, H: int, S: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """The two generated keep-bit layouts as [B*H, S, S] 0/1 int64 tensors (query, key): A (key
+    bits per query word) and B (query bits per key word) -- both must equal attn_keep_mask."""
+    W = (S + 31) // 32
+    m = masks.cpu().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    pos = _lm_pos(S)
+    bits = torch.arange(32, dtype=torch.int64)
+    out = []
+    for li in range(2):
+        words = m[li].view(B * H, W, 32 * W)[:, :, pos]          # [bh][w][position]
+        d = ((words.unsqueeze(-1) >> bits) & 1).permute(0, 2, 1, 3).reshape(B * H, S, W * 32)[..., :S]
+        out.append(d if li == 0 else d.transpose(1, 2))            # B: [bh][key][q] -> [bh][q][key]
+    return out[0], out[1]
+
+
 class PendingMasks:
     """Dropout keep-bit masks being generated on a side stream (see ``attn_masks_async``)."""
 
@@ -133,8 +162,7 @@ def attn_masks_async(B, S, H, D, p, rng: RngState, sid, device) -> PendingMasks 
             or not _lib.has("dtd_attn_masks"):
         return None
     cur = torch.cuda.current_stream(device)
-    W = (S + 31) // 32
-    masks = torch.empty((2, B * H * S * W), dtype=torch.int32, device=device)
+    masks = torch.empty((2, mask_words(B, H, S)), dtype=torch.int32, device=device)
     side = _side_stream(torch.device(device))
     side.wait_stream(cur)                      # the rng step / previous users of the buffer
     with torch.cuda.stream(side):
@@ -163,8 +191,7 @@ def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | 
         torch.cuda.current_stream(qkv.device).wait_event(masks.event)
         masks, rng_ptr = masks.masks, None     # generated already
     elif p > 0:
-        W = (S + 31) // 32
-        masks = torch.empty((2, B * H * S * W), dtype=torch.int32, device=qkv.device)
+        masks = torch.empty((2, mask_words(B, H, S)), dtype=torch.int32, device=qkv.device)
     else:
         masks = None
     sl = slopes.to(device=qkv.device, dtype=torch.float32).contiguous() if slopes is not None else None

@@ -149,9 +149,28 @@ __device__ __forceinline__ float keep_of(const DropoutRng& g, uint64_t e, uint32
   return h16 >= thr ? 1.f : 0.f;
 }
 
+// Keep-word layout.  Both mask layouts hold [B*H][W][Sp] words (Sp = 32 W) with the words of each
+// 32-position group permuted: the word of position 32g + c sits at 32g + lm_pos(c), c = 8a + 4b + j
+// -> 8a + 2j + b.  The words of positions c and c + 4 (b = 0) -- the two rows one accumulator
+// register of a 32x32 MFMA tile holds in its lower / upper 32 lanes (crow(i, 0), crow(i, 1)) -- are
+// then adjacent: register i's 64-lane keep mask is the aligned 64-bit word i of the group, one
+// scalar load away, and a keep is ONE v_cndmask_b32 with that SGPR pair (attn_fwd_kernel).
+__device__ __forceinline__ int lm_pos(int x) {
+  const int c = x & 31;
+  return (x & ~31) | (c & 24) | ((c & 3) << 1) | ((c >> 2) & 1);
+}
+// v ? keep : 0 for the lane's bit of a wave-uniform 64-bit mask held in an SGPR pair
+__device__ __forceinline__ float sel_keep(float v, uint64_t m) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
+  return r;
+}
+typedef __attribute__((address_space(4))) const uint64_t cu64;
+
 struct FwdArgs {
   const bf16* q; const bf16* k; const bf16* v; bf16* o; float* lse; const float* slopes;
-  const uint32_t* maskA;  // dropout keep bits [B*H][W][S]: bit j of word (w, q) = key 32w+j  (nullptr: no dropout)
+  const uint32_t* maskA;  // dropout keep bits [B*H][W][Sp]: bit j of word (w, q) = key 32w+j  (nullptr: no dropout)
+  const uint32_t* maskB;  // [B*H][W][Sp]: bit j of word (w, key) = query 32w+j
   int B, S, H, ld, ldo, causal, W;
   float scale, p, thr;
 };
@@ -204,9 +223,9 @@ __global__ void __launch_bounds__(256) attn_mask_kernel(uint32_t* __restrict__ m
     }
     const int nk = S - kw * 32;                  // valid keys in this word
     if (nk < 32) word &= (0xffffffffu >> (32 - nk));
-    if (qv) maskA[((size_t)bh * W + kw) * S + q] = word;
+    if (qv) maskA[((size_t)bh * W + kw) * (32 * W) + lm_pos(q)] = word;
     const int key = kw * 32 + (lane & 31);
-    if (key < S && qw < W) maskB[((size_t)bh * W + qw) * S + key] = bw;
+    if (key < S && qw < W) maskB[((size_t)bh * W + qw) * (32 * W) + lm_pos(key)] = bw;
   }
 }
 
@@ -257,7 +276,7 @@ __global__ void __launch_bounds__(256) attn_mask_kernel_t(uint32_t* __restrict__
     word = __builtin_bitreverse32(word);
     const int nk = S - kw * 32;                  // valid keys in this word
     if (nk < 32) word &= (0xffffffffu >> (32 - nk));
-    if (qv) maskA[((size_t)bh * W + kw) * S + q] = word;
+    if (qv) maskA[((size_t)bh * W + kw) * (32 * W) + lm_pos(q)] = word;
     uint32_t t = word;
     t = swap_stage<16>(t, sh[0], mk[0]);
     t = swap_stage<8>(t, sh[1], mk[1]);
@@ -265,7 +284,7 @@ __global__ void __launch_bounds__(256) attn_mask_kernel_t(uint32_t* __restrict__
     t = swap_stage<2>(t, sh[3], mk[3]);
     t = swap_stage<1>(t, sh[4], mk[4]);
     const int key = kw * 32 + (lane & 31);
-    if (key < S && qw < W) maskB[((size_t)bh * W + qw) * S + key] = t;
+    if (key < S && qw < W) maskB[((size_t)bh * W + qw) * (32 * W) + lm_pos(key)] = t;
   }
 }
 
@@ -322,11 +341,12 @@ struct WordSrc {
     return __builtin_amdgcn_raw_buffer_load_b32(rs, voff, wi * stride, 0);
   }
 };
-__device__ __forceinline__ WordSrc word_src(const uint32_t* words, const void* dummy, int W, int S, int pos) {
+__device__ __forceinline__ WordSrc word_src(const uint32_t* words, const void* dummy, int W, int pos) {
   WordSrc w;
-  w.rs = bounded_rsrc(words ? (const void*)words : dummy, words ? (uint32_t)W * S * 4u : 0u);
-  w.voff = pos * 4;
-  w.stride = S * 4;
+  const int Sp = 32 * W;
+  w.rs = bounded_rsrc(words ? (const void*)words : dummy, words ? (uint32_t)W * Sp * 4u : 0u);
+  w.voff = lm_pos(pos) * 4;
+  w.stride = Sp * 4;
   return w;
 }
 
@@ -383,7 +403,8 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * VP];
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, r = lane & 31;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5,
+            r = lane & 31;
   int tx, ty;
   xcd_tile(tx, ty);
   const int bh = ty, b = bh / a.H, h = bh % a.H;
@@ -397,7 +418,12 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
   const RowSrc ksrc = row_src<D>(a.k + (size_t)b * S * a.ld + h * D, a.ld, S);
   const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
-  const WordSrc wsrc = word_src(drop ? a.maskA + (size_t)bh * a.W * S : nullptr, a.lse, a.W, S, qvalid ? q : 0);
+  // dropout: this wave's 32 queries are one query word of the key-major layout, so the keep masks
+  // of a 32-key block are 16 aligned 64-bit words (lm_pos) -- scalar loads, one v_cndmask per
+  // score.  A one-dword-per-lane vector load of the same 64 words a tile ahead pulls them into L2.
+  const int Sp = 32 * a.W;
+  const uint32_t* mrow = drop ? a.maskB + ((size_t)bh * a.W + (q0 >> 5)) * Sp : nullptr;
+  const __amdgpu_buffer_rsrc_t mrs = bounded_rsrc(drop ? (const void*)mrow : (const void*)a.lse, drop ? (uint32_t)Sp * 4u : 0u);
 
   bf16x8 qf[NC];
   {
@@ -421,22 +447,20 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   TileLoader<D, BN> kl0, vl0, kl1r, vl1r;
   TileLoader<D, BN>& kl1 = RING == 2 ? kl1r : kl0;
   TileLoader<D, BN>& vl1 = RING == 2 ? vl1r : vl0;
-  uint32_t mwc[NKB], mw0[NKB], mw1r[NKB];
-  uint32_t* mw1 = RING == 2 ? mw1r : mw0;
-  // unconditional word loads (zeros without dropout) keep the ring branch-free
-  auto load_words = [&](int k0, uint32_t* out) {
-#pragma unroll
-    for (int j = 0; j < NKB; ++j) out[j] = wsrc.load((k0 >> 5) + j);
+  uint32_t pf0 = 0, pf1r = 0;   // L2 prefetch of keep words (value unused)
+  uint32_t& pf1 = RING == 2 ? pf1r : pf0;
+  auto prefetch_words = [&](int k0, uint32_t& out) {
+    asm volatile("" :: "v"(out));   // retire the previous prefetch held in this register
+    out = __builtin_amdgcn_raw_buffer_load_b32(mrs, lane * 4, k0 * 4, 0);
   };
-  load_words(0, mwc);
   kl0.load(ksrc, 0);
   vl0.load(vsrc, 0);
   kl0.store(Ks[0], KP);
   vl0.store(Vs[0], VP);
   {
     const int k1 = min(1, nt - 1) * BN, k2 = min(2, nt - 1) * BN;
-    kl1.load(ksrc, k1); vl1.load(vsrc, k1); load_words(k1, mw1);
-    if constexpr (RING == 2) { kl0.load(ksrc, k2); vl0.load(vsrc, k2); load_words(k2, mw0); }
+    kl1.load(ksrc, k1); vl1.load(vsrc, k1); prefetch_words(k1, pf1);
+    if constexpr (RING == 2) { kl0.load(ksrc, k2); vl0.load(vsrc, k2); prefetch_words(k2, pf0); }
   }
   __syncthreads();
   // SET = register set holding tile t+1 (t even -> 1, t odd -> 0)
@@ -444,10 +468,18 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     constexpr int SET = decltype(set_c)::value;
     TileLoader<D, BN>& kn = SET ? kl1 : kl0;
     TileLoader<D, BN>& vn = SET ? vl1 : vl0;
-    uint32_t* mwn = SET ? mw1 : mw0;
+    uint32_t& pfn = SET ? pf1 : pf0;
     const int buf = t & 1, k0 = t * BN;
     const bf16* K = Ks[buf];
     const bf16* V = Vs[buf];
+    // keep masks of the tile's first 32-key block: issued ahead of the score MFMAs (their L2
+    // round trip hides under the QK^T / softmax work); the next block's after this one's selects
+    uint64_t mk[16];
+    auto load_masks = [&](int kb) {
+      const cu64* mp = (const cu64*)(uintptr_t)(mrow + k0 + kb * 32);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mk[i] = mp[i];
+    };
     f32x16 sacc[NKB];
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
@@ -457,6 +489,10 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
         acc = mfma32(*reinterpret_cast<const bf16x8*>(&K[(kb * 32 + r) * KP + 16 * c + 8 * hh]), qf[c], acc);
       sacc[kb] = acc;
     }
+    // the first block's keep masks: issued once the score MFMAs' LDS operands are consumed (an
+    // outstanding scalar load makes every later LDS wait a full lgkmcnt(0)), landing under the
+    // max / exp work
+    if (drop) load_masks(0);
     // log2-domain scores.  Fast path (no ALiBi, interior tile): the row max is taken on the raw
     // accumulator (scale > 0) and the scale is folded into the exponent's FMA -- 4 VALU per score
     // incl. the running sum, vs 10+ with a per-element scale/bias/mask pass.
@@ -527,9 +563,9 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     if (drop) {
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
-        const uint32_t mw = half_word(mwc[kb], hh);
+        if (kb > 0) load_masks(kb);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[kb][i] = keep_bits(sacc[kb][i], mw, crow(i, 0));
+        for (int i = 0; i < 16; ++i) sacc[kb][i] = sel_keep(sacc[kb][i], mk[i]);
       }
     }
     // O^T += V^T . P^T: the score accumulator is the B operand; V^T comes from transposed reads
@@ -546,13 +582,11 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     if (t + 1 < nt) {
       kn.store(Ks[buf ^ 1], KP);
       vn.store(Vs[buf ^ 1], VP);
-#pragma unroll
-      for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
       // tile t+1+RING (clamped to the last tile: a harmless reload keeps the issue unconditional)
       const int kf = min(t + 1 + RING, nt - 1) * BN;
       kn.load(ksrc, kf);
       vn.load(vsrc, kf);
-      load_words(kf, mwn);
+      prefetch_words(kf, pfn);
     }
     __syncthreads();
   };
@@ -605,7 +639,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_pipe_kernel(FwdArgs a) {
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
   const RowSrc ksrc = row_src<D>(a.k + (size_t)b * S * a.ld + h * D, a.ld, S);
   const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
-  const WordSrc wsrc = word_src(drop ? a.maskA + (size_t)bh * a.W * S : nullptr, a.lse, a.W, S, qvalid ? q : 0);
+  const WordSrc wsrc = word_src(drop ? a.maskA + (size_t)bh * a.W * (32 * a.W) : nullptr, a.lse, a.W, qvalid ? q : 0);
 
   bf16x8 qf[NC];
   {
@@ -833,7 +867,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   constexpr bool drop = DROP;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
   const float kbias = sl2 * (float)key;   // ALiBi bias of this lane's key (0 without ALiBi)
-  const WordSrc wsrc = word_src(drop ? a.maskB + (size_t)bh * a.W * S : nullptr, a.lse, a.W, S, kvalid ? key : 0);
+  const WordSrc wsrc = word_src(drop ? a.maskB + (size_t)bh * a.W * (32 * a.W) : nullptr, a.lse, a.W, kvalid ? key : 0);
   const RowSrc qsrc = row_src<D>(a.q + (size_t)b * S * a.ld + h * D, a.ld, S);
   const RowSrc osrc = row_src<D>(a.dout + (size_t)b * S * a.ldo + h * D, a.ldo, S);
   const float* lseb = a.lse + (size_t)bh * S;
@@ -1041,7 +1075,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
   const RowSrc ksrc = row_src<D>(a.k + (size_t)b * S * a.ld + h * D, a.ld, S);
   const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
-  const WordSrc wsrc = word_src(drop ? a.maskA + (size_t)bh * a.W * S : nullptr, a.lse, a.W, S, qvalid ? q : 0);
+  const WordSrc wsrc = word_src(drop ? a.maskA + (size_t)bh * a.W * (32 * a.W) : nullptr, a.lse, a.W, qvalid ? q : 0);
 
   bf16x8 qf[NC], of[NC];
   {
@@ -1263,7 +1297,8 @@ static int tile_keys(int which) {
 // The tile loads address one (batch, head)'s rows through 32-bit buffer offsets (RowSrc).
 static bool offsets_fit(int S, int ld, int ldo) {
   const long long lim = 0x7fffffffLL;
-  return (long long)S * ld * 2 < lim && (long long)S * ldo * 2 < lim && (long long)S * ((S + 31) / 32) * 4 < lim;
+  const long long W = (S + 31) / 32;
+  return (long long)S * ld * 2 < lim && (long long)S * ldo * 2 < lim && 32 * W * W * 4 < lim;
 }
 
 DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const float* slopes,
@@ -1279,14 +1314,15 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
     // rng == nullptr: the masks were generated ahead of time by dtd_attn_masks (on a side
     // stream, overlapping the QKV GEMM)
     if (rng) {
-      uint32_t* mB = masks + (size_t)B * H * S * W;
+      uint32_t* mB = masks + (size_t)B * H * (32 * W) * W;
       hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : attn_mask_kernel_t, dim3((S + 63) / 64, B * H), dim3(256), 0,
                          s, mA, mB, S, W, rng, sid, keep_threshold(p));
     }
   }
   const char* thr_env = getenv("DTD_ATTN_RESCALE_THR");
   const float thr = thr_env ? (float)atof(thr_env) : kRescaleThr;
-  FwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, slopes, mA, B, S, H, ld, ldo, causal, W,
+  const uint32_t* mBk = mA ? mA + (size_t)B * H * (32 * W) * W : nullptr;
+  FwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, lse, slopes, mA, mBk, B, S, H, ld, ldo, causal, W,
             scale, p, thr};
   dim3 grid((S + 127) / 128, B * H);
   if (D == 64 && fwd_pipe()) {
@@ -1314,7 +1350,7 @@ DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, con
   if (!masks || !rng) return (int)hipErrorInvalidValue;
   const int W = (S + 31) / 32;
   hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : attn_mask_kernel_t, dim3((S + 63) / 64, B * H), dim3(256), 0, s,
-                     masks, masks + (size_t)B * H * S * W, S, W, rng, sid, keep_threshold(p));
+                     masks, masks + (size_t)B * H * (32 * W) * W, S, W, rng, sid, keep_threshold(p));
   DTD_LAUNCH_CHECK();
 }
 
@@ -1337,7 +1373,7 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   if (!offsets_fit(S, ld, ldo)) return (int)hipErrorInvalidValue;
   const int W = (S + 31) / 32;
   const uint32_t* mA = (p > 0.f) ? masks : nullptr;
-  const uint32_t* mB = (p > 0.f) ? masks + (size_t)B * H * S * W : nullptr;
+  const uint32_t* mB = (p > 0.f) ? masks + (size_t)B * H * (32 * W) * W : nullptr;
   if (p > 0.f && !masks) return (int)hipErrorInvalidValue;
   dim3 grid((S + 127) / 128, B * H);
   BwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (const bf16*)o,
