@@ -854,7 +854,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   auto& Qs = sm.Qs;
   auto& Os = sm.Os;
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, r = lane & 31;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5,
+            r = lane & 31;
   int tx, ty;
   xcd_tile(tx, ty);
   const int bh = ty, b = bh / a.H, h = bh % a.H;
@@ -867,7 +868,11 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   constexpr bool drop = DROP;
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
   const float kbias = sl2 * (float)key;   // ALiBi bias of this lane's key (0 without ALiBi)
-  const WordSrc wsrc = word_src(drop ? a.maskB + (size_t)bh * a.W * (32 * a.W) : nullptr, a.lse, a.W, kvalid ? key : 0);
+  // keep masks: this wave's 32 keys are one key word of the query-major layout A, so a 32-query
+  // block's masks are 16 aligned 64-bit words (lm_pos) -- scalar loads, one v_cndmask per use
+  const int Sp = 32 * a.W;
+  const uint32_t* mrow = drop ? a.maskA + ((size_t)bh * a.W + ((kblk >> 5) + w)) * Sp : nullptr;
+  const __amdgpu_buffer_rsrc_t mrs = bounded_rsrc(drop ? (const void*)mrow : (const void*)a.lse, drop ? (uint32_t)Sp * 4u : 0u);
   const RowSrc qsrc = row_src<D>(a.q + (size_t)b * S * a.ld + h * D, a.ld, S);
   const RowSrc osrc = row_src<D>(a.dout + (size_t)b * S * a.ldo + h * D, a.ldo, S);
   const float* lseb = a.lse + (size_t)bh * S;
@@ -897,21 +902,19 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       del_r = qq < S ? -delb[qq] : 0.f;            //                 dS = P (dP - delta)
     }
   };
-  // dropout keep words of a query tile (one per 32 query rows), prefetched a tile ahead with
-  // the Q/dO loads so their global-load latency is never waited on inside the tile
-  constexpr int NQW = BM / 32;
-  uint32_t mwc[NQW], mwn[NQW];
-  auto load_words = [&](int q0, uint32_t* out) {
+  // L2 prefetch of the next query tile's keep words (BM words, value unused)
+  constexpr int NPF = BM / 64;
+  uint32_t pfw[NPF] = {};
+  auto prefetch_words = [&](int q0) {
 #pragma unroll
-    for (int j = 0; j < NQW; ++j) {
-      const int qw = (q0 >> 5) + j;
-      out[j] = drop ? wsrc.load(qw) : 0u;
+    for (int j = 0; j < NPF; ++j) {
+      asm volatile("" :: "v"(pfw[j]));
+      pfw[j] = __builtin_amdgcn_raw_buffer_load_b32(mrs, (lane + 64 * j) * 4, q0 * 4, 0);
     }
   };
   ql.load(qsrc, qstart);
   ol.load(osrc, qstart);
   load_stats(qstart);
-  load_words(qstart, mwc);
   ql.store_bwd(Qs[0], QP);
   ol.store_bwd(Os[0], QP);
   if (threadIdx.x < BM) { lse_s[0][threadIdx.x] = lse_r; del_s[0][threadIdx.x] = del_r; }
@@ -922,7 +925,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       ql.load(qsrc, q0 + BM);
       ol.load(osrc, q0 + BM);
       load_stats(q0 + BM);
-      load_words(q0 + BM, mwn);
+      if (drop) prefetch_words(q0 + BM);
     }
     const bf16* Q = Qs[buf];
     const bf16* O = Os[buf];
@@ -946,10 +949,13 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       const int qrow0 = q0 + qb * 32;
       // block-uniform predicate (a scalar branch, never a per-element one)
       const bool needmask = (kblk + 128 > S) || (qrow0 + 32 > S) || (a.causal && kblk + 127 > qrow0);
-      uint32_t mw = mwc[0];
+      // this query block's keep masks (after the S / dP MFMAs consumed their LDS operands)
+      uint64_t mk[16];
+      if constexpr (DROP) {
+        const cu64* mp = (const cu64*)(uintptr_t)(mrow + qrow0);
 #pragma unroll
-      for (int j = 1; j < NQW; ++j) mw = qb == j ? mwc[j] : mw;   // register select, no scratch
-      mw = half_word(mw, hh);
+        for (int i = 0; i < 16; ++i) mk[i] = mp[i];
+      }
       // row statistics of this lane's 16 accumulator rows (rows 8g + 4hh + 0..3 are contiguous):
       // 8 ds_read_b128 issued together instead of 32 dependent scalar LDS reads
       f32x4 L4[4], D4[4];
@@ -980,14 +986,13 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       for (int i = 0; i < 16; i += 2) {
         const f32x2 nd = pk2(D4[i >> 2][i & 3], D4[i >> 2][(i & 3) + 1]);
         if constexpr (DROP) {
-          const int m0 = bit_mask(mw, crow(i, 0));
-          const int m1 = bit_mask(mw, crow(i + 1, 0));
-          const f32x2 t = pk_fma(pk2(mask_bits(pacc[i], m0), mask_bits(pacc[i + 1], m1)), pk2(inv_keep, inv_keep), nd);
+          const f32x2 t = pk_fma(pk2(sel_keep(pacc[i], mk[i]), sel_keep(pacc[i + 1], mk[i + 1])),
+                                 pk2(inv_keep, inv_keep), nd);
           const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * t;                 // dS
           pacc[i] = ds.x;
           pacc[i + 1] = ds.y;
-          sacc[i] = mask_bits(sacc[i], m0);                               // P*mask (dV)
-          sacc[i + 1] = mask_bits(sacc[i + 1], m1);
+          sacc[i] = sel_keep(sacc[i], mk[i]);                             // P*mask (dV)
+          sacc[i + 1] = sel_keep(sacc[i + 1], mk[i + 1]);
         } else {
           const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * (pk2(pacc[i], pacc[i + 1]) + nd);
           pacc[i] = ds.x;
@@ -1015,8 +1020,6 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       ql.store_bwd(Qs[buf ^ 1], QP);
       ol.store_bwd(Os[buf ^ 1], QP);
       if (threadIdx.x < BM) { lse_s[buf ^ 1][threadIdx.x] = lse_r; del_s[buf ^ 1][threadIdx.x] = del_r; }
-#pragma unroll
-      for (int j = 0; j < NQW; ++j) mwc[j] = mwn[j];
     }
     __syncthreads();
   }
@@ -1061,7 +1064,8 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * KP];
   __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * KP];
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, r = lane & 31;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5,
+            r = lane & 31;
   int tx, ty;
   xcd_tile(tx, ty);
   const int bh = ty, b = bh / a.H, h = bh % a.H;
@@ -1075,7 +1079,10 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   const float inv_keep = drop ? 1.f / (1.f - a.p) : 1.f;
   const RowSrc ksrc = row_src<D>(a.k + (size_t)b * S * a.ld + h * D, a.ld, S);
   const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
-  const WordSrc wsrc = word_src(drop ? a.maskA + (size_t)bh * a.W * (32 * a.W) : nullptr, a.lse, a.W, qvalid ? q : 0);
+  // keep masks as in attn_fwd_kernel: 64-bit lane masks of the key-major layout, scalar loads
+  const int Sp = 32 * a.W;
+  const uint32_t* mrow = drop ? a.maskB + ((size_t)bh * a.W + (q0 >> 5)) * Sp : nullptr;
+  const __amdgpu_buffer_rsrc_t mrs = bounded_rsrc(drop ? (const void*)mrow : (const void*)a.lse, drop ? (uint32_t)Sp * 4u : 0u);
 
   bf16x8 qf[NC], of[NC];
   {
@@ -1116,29 +1123,27 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   TileLoader<D, BN> kl0, vl0, kl1r, vl1r;
   TileLoader<D, BN>& kl1 = RING == 2 ? kl1r : kl0;
   TileLoader<D, BN>& vl1 = RING == 2 ? vl1r : vl0;
-  uint32_t mwc[NKB], mw0[NKB], mw1r[NKB];
-  uint32_t* mw1 = RING == 2 ? mw1r : mw0;
-  // unconditional word loads (zeros without dropout) keep the ring branch-free
-  auto load_words = [&](int k0, uint32_t* out) {
-#pragma unroll
-    for (int j = 0; j < NKB; ++j) out[j] = wsrc.load((k0 >> 5) + j);
+  uint32_t pf0 = 0, pf1r = 0;   // L2 prefetch of keep words (value unused)
+  uint32_t& pf1 = RING == 2 ? pf1r : pf0;
+  auto prefetch_words = [&](int k0, uint32_t& out) {
+    asm volatile("" :: "v"(out));
+    out = __builtin_amdgcn_raw_buffer_load_b32(mrs, lane * 4, k0 * 4, 0);
   };
-  load_words(0, mwc);
   kl0.load(ksrc, 0);
   vl0.load(vsrc, 0);
   kl0.store_bwd(Ks[0], KP);
   vl0.store_bwd(Vs[0], KP);
   {
     const int k1 = min(1, nt - 1) * BN, k2 = min(2, nt - 1) * BN;
-    kl1.load(ksrc, k1); vl1.load(vsrc, k1); load_words(k1, mw1);
-    if constexpr (RING == 2) { kl0.load(ksrc, k2); vl0.load(vsrc, k2); load_words(k2, mw0); }
+    kl1.load(ksrc, k1); vl1.load(vsrc, k1); prefetch_words(k1, pf1);
+    if constexpr (RING == 2) { kl0.load(ksrc, k2); vl0.load(vsrc, k2); prefetch_words(k2, pf0); }
   }
   __syncthreads();
   auto tile = [&](auto set_c, int t) {
     constexpr int SET = decltype(set_c)::value;
     TileLoader<D, BN>& kn = SET ? kl1 : kl0;
     TileLoader<D, BN>& vn = SET ? vl1 : vl0;
-    uint32_t* mwn = SET ? mw1 : mw0;
+    uint32_t& pfn = SET ? pf1 : pf0;
     const int buf = t & 1, k0 = t * BN;
     const bf16* K = Ks[buf];
     const bf16* V = Vs[buf];
@@ -1156,7 +1161,13 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
           pacc = mfma32(*reinterpret_cast<const bf16x8*>(&V[(kb * 32 + r) * KP + 16 * c + 8 * hh]), of[c], pacc);
         }
       }
-      const uint32_t mw = half_word(mwc[kb], hh);
+      // this block's keep masks (after the S / dP MFMAs consumed their LDS operands)
+      uint64_t mk[16];
+      if (drop) {
+        const cu64* mp = (const cu64*)(uintptr_t)(mrow + k0 + kb * 32);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mk[i] = mp[i];
+      }
       // P = exp2(s*log2e - lse): 2 VALU on interior tiles without ALiBi
       if (needmask || sl2 != 0.f) {
 #pragma unroll
@@ -1184,14 +1195,14 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
           f32x2 dp = pk2(pacc[i], pacc[i + 1]);
-          if (drop) dp = pk2(keep_bits(pacc[i], mw, crow(i, 0)), keep_bits(pacc[i + 1], mw, crow(i + 1, 0)));
+          if (drop) dp = pk2(sel_keep(pacc[i], mk[i]), sel_keep(pacc[i + 1], mk[i + 1]));
           const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * pk_fma(dp, ik2, nd2);
           sacc[i] = ds.x;
           sacc[i + 1] = ds.y;
         }
       } else if (drop) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[i] *= fmaf(keep_bits(pacc[i], mw, crow(i, 0)), inv_keep, -dl);
+        for (int i = 0; i < 16; ++i) sacc[i] *= fmaf(sel_keep(pacc[i], mk[i]), inv_keep, -dl);
       } else {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[i] *= pacc[i] - dl;
@@ -1211,13 +1222,11 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
     if (t + 1 < nt) {
       kn.store_bwd(Ks[buf ^ 1], KP);
       vn.store_bwd(Vs[buf ^ 1], KP);
-#pragma unroll
-      for (int j = 0; j < NKB; ++j) mwc[j] = mwn[j];
       // tile t+1+RING (clamped to the last tile: a harmless reload keeps the issue unconditional)
       const int kf = min(t + 1 + RING, nt - 1) * BN;
       kn.load(ksrc, kf);
       vn.load(vsrc, kf);
-      load_words(kf, mwn);
+      prefetch_words(kf, pfn);
     }
     __syncthreads();
   };
