@@ -204,6 +204,45 @@ __device__ __forceinline__ bf16x4 cvt4(f32x4 v) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3);
 }
 
+// act(x) and act'(x) of 8 values stage by stage (each stage's 8 independent operations next to
+// each other, so the dependent chain of one value never stalls on an instruction-latency hazard);
+// the same arithmetic, operation for operation, as epi_act_and_grad
+template <int EPI>
+__device__ __forceinline__ void act_and_grad8(const bf16x8& v, float (&a)[8], float (&d)[8]) {
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (float)v[j];
+  if constexpr (EPI == EPI_BIAS_GELU_TANH_G) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) epi_act_and_grad<EPI>(x[j], a[j], d[j]);
+  } else {
+    float e[8], t[8], p[8], c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = gauss_e(x[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = __builtin_amdgcn_rcpf(fmaf(fabsf(x[j]), 0.3275911f * 0.70710678118654752f, 1.f));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = fmaf(t[j], 1.061405429f, -1.453152027f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = fmaf(t[j], p[j], 1.421413741f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = fmaf(t[j], p[j], -0.284496736f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = t[j] * fmaf(t[j], p[j], 0.254829592f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = 0.5f + 0.5f * copysignf(1.f - p[j] * e[j], x[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = x[j] * c[j];
+      d[j] = fmaf(x[j] * 0.3989422804014327f, e[j], c[j]);
+    }
+  }
+}
+__device__ __forceinline__ bf16x8 cvt8(const float (&f)[8]) {
+  const bf16x4 lo = cvt4(f32x4{f[0], f[1], f[2], f[3]}), hi = cvt4(f32x4{f[4], f[5], f[6], f[7]});
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // bijective XCD remap of the linear workgroup id (dispatch deals ids round-robin over 8 XCDs):
 // each XCD gets a contiguous range of tiles, so tiles sharing an A panel share an L2
 __device__ __forceinline__ int xcd_remap(int id, int n) {
@@ -424,16 +463,10 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_kernel(GemmArgs g) {
     if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
       *reinterpret_cast<bf16x8*>(g.c + off) = v;
     } else if constexpr (stores_grad(EPI)) {
-      bf16x8 a, d;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float aj, dj;
-        epi_act_and_grad<EPI>((float)v[j], aj, dj);
-        a[j] = (bf16)aj;
-        d[j] = (bf16)dj;
-      }
-      *reinterpret_cast<bf16x8*>(g.c + off) = d;
-      *reinterpret_cast<bf16x8*>(g.c2 + off) = a;
+      float a[8], d[8];
+      act_and_grad8<EPI>(v, a, d);
+      *reinterpret_cast<bf16x8*>(g.c + off) = cvt8(d);
+      *reinterpret_cast<bf16x8*>(g.c2 + off) = cvt8(a);
     } else if constexpr (is_gelu_fwd(EPI)) {
       bf16x8 a;
 #pragma unroll
@@ -932,16 +965,10 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
         if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
           *reinterpret_cast<bf16x8*>(g.c + off) = v;
         } else if constexpr (stores_grad(EPI)) {
-          bf16x8 av, dv;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float aj, dj;
-            epi_act_and_grad<EPI>((float)v[j], aj, dj);
-            av[j] = (bf16)aj;
-            dv[j] = (bf16)dj;
-          }
-          *reinterpret_cast<bf16x8*>(g.c + off) = dv;
-          *reinterpret_cast<bf16x8*>(g.c2 + off) = av;
+          float av[8], dv[8];
+          act_and_grad8<EPI>(v, av, dv);
+          *reinterpret_cast<bf16x8*>(g.c + off) = cvt8(dv);
+          *reinterpret_cast<bf16x8*>(g.c2 + off) = cvt8(av);
         } else if constexpr (is_gelu_fwd(EPI)) {
           bf16x8 av;
 #pragma unroll
@@ -949,14 +976,13 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
           *reinterpret_cast<bf16x8*>(g.c + off) = v;
           *reinterpret_cast<bf16x8*>(g.c2 + off) = av;
         } else {
-          bf16x8 o;
+          float o[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float du = (float)v[j] * epi_act_grad<EPI>((float)uin[rr][i][j]);
-            o[j] = (bf16)du;
-            colsum[j] += du;
+            o[j] = (float)v[j] * epi_act_grad<EPI>((float)uin[rr][i][j]);
+            colsum[j] += o[j];
           }
-          *reinterpret_cast<bf16x8*>(g.c + off) = o;
+          *reinterpret_cast<bf16x8*>(g.c + off) = cvt8(o);
         }
       }
       if (dyn && rr == 1 && tid == 0) qslot[(it + 1) & 1] = has_next ? beg + 2 * per + claim : end;
