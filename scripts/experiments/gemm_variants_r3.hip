@@ -998,3 +998,228 @@ __global__ void __launch_bounds__(256, 1) gemm_bt_w4(GemmArgs g) {
 // middle of the MFMA segment 0.78x; no s_setprio around the MFMA segments 0.90x; both 0.75x; one
 // barrier per phase without the wave-row stagger 0.95x.  The shipped order (reads, then DMA, then
 // the counted wait and barrier; MFMA segment at priority 1) is the best of the set.
+
+// ---------------------------------------------------------------------------------------------
+// Round 3b: W4R -- the 4-wave (one per SIMD, 128x128 per wave) form with the operands staged
+// through registers instead of LDS-DMA (the LDS-DMA issue cost the W4 form could not hide).
+// Built into gemm.hip as DTD_GEMM_VARIANT=4 for EPI_STORE, launched like the persistent kernel
+// (nwg workgroups of 256 threads):
+//     if (gemm_variant() == 4 && epi == EPI_STORE && K / BK >= 2) {
+//       if (bias) hipLaunchKernelGGL((gemm_bt_w4r<true>), dim3(nwg), dim3(256), 0, s, g);
+//       else hipLaunchKernelGGL((gemm_bt_w4r<false>), dim3(nwg), dim3(256), 0, s, g);
+//     }
+// Correct (scripts/bench_gemm_v2.py checks, tests/test_gemm_gpu.py 39 passed under it).  Timing
+// (VNEW=4 scripts/bench_gemm_v2.py, same box): first version with the staging / next-step reads
+// behind runtime conditions 0.57-0.69x v1 (the branches split the K-step into basic blocks, so the
+// sched_group_barrier interleave did not apply: reads, stores and loads clumped beside idle MFMA
+// issue); branch-free K-step 0.79-0.89x v1 (e.g. fwd qkv 507 vs 438 us, fc2 542 vs 464 us,
+// hipBLASLt 388 / 437).  512 VGPRs (256 accumulators, 128 for the double-buffered X / Y
+// fragments, 32 staging): the half-K-step staging ring leaves each load one MFMA part (~1 k cycles)
+// before its ds_write, and a lone wave stalls its whole MFMA stream on that vmcnt.  Next step if
+// revisited: stream the A fragments per 16-row block (8 instead of 32 registers per k-half), which
+// frees the registers for a full K-step staging ring (two parts of load distance).
+// // ---------------------------------------------------------------------------------------------
+// // W4R form (DTD_GEMM_VARIANT=4; EPI_STORE, optional bias; K >= 128): FOUR waves, one per SIMD,
+// // each owning a 128 x 128 quarter of the 256 x 256 tile in 256 fp32 accumulators (a wave alone on
+// // its SIMD may use the whole 512-entry register file).  Per K-step a wave reads 32 fragments for
+// // 128 MFMAs (0.25 reads per MFMA against 0.375 in the 8-wave form) and the operands are staged
+// // through REGISTERS: 16 global loads into 64 VGPRs and 16 ds_write_b128 a K-step later -- the
+// // 8-wave form's limiter is the ~90-cycle issue of each buffer_load...lds (profiles/
+// // r3_gemm_limiter_probe.jsonl), and one wave per SIMD has no partner to hide it behind (the
+// // LDS-DMA version of this schedule ran 0.65-0.80x, scripts/experiments/gemm_variants_r3.hip).
+// //   K-step g (buffer g & 1): part 1 = MFMAs of k-half 0 (fragments X) beside the k-half 1 reads
+// //   (Y); barrier; part 2 = MFMAs of k-half 1 (Y) beside the k-half 0 reads of K-step g + 1 (X), the
+// //   LDS stores of K-step g + 2 into buffer g & 1 (read out in part 1) and the global loads of
+// //   K-step g + 3.  One barrier per K-step plus one per part boundary.
+// // The staging image is the LDS-DMA one (lane-linear 1 KiB pieces, source-side chunk swizzle), so
+// // the fragment reads are those of the 8-wave kernel.  Persistent XCD-grouped static tile order;
+// // a tile's epilogue stores 16-byte row pieces straight from the accumulators (v_permlane16_swap).
+// constexpr int W4R_LDS = LDS_BYTES + 1024;
+//
+// struct W4Ctx {
+//   int voff;           // per-lane source offset (row L/8 of an 8-row piece, swizzled chunk)
+//   int abase, bbase;   // per-lane fragment read offsets within a K-step buffer (chunk of k-half 0)
+//   int kh1;            // byte delta from the k-half 0 chunk to the k-half 1 chunk
+//   int w, wm, wn, li, lq, lane;
+// };
+//
+// // half H (8 of this wave's 16 pieces, 1 KiB each) of K-step `kk` of the operand panel `rs` ->
+// // registers, and registers -> the lane-linear LDS image of a K-step buffer
+// __device__ __forceinline__ void w4r_load(const W4Ctx& C, __amdgpu_buffer_rsrc_t rs, int ld, int kk, int H,
+//                                          bf16x8 (&st)[8]) {
+// #pragma unroll
+//   for (int i = 0; i < 8; ++i)
+//     st[i] = __builtin_bit_cast(bf16x8,
+//                                __builtin_amdgcn_raw_buffer_load_b128(rs, C.voff, kk * BK * 2 + (H * 8 + i) * 16 * ld, 0));
+// }
+// __device__ __forceinline__ void w4r_write(const W4Ctx& C, char* buf, int H, const bf16x8 (&st)[8]) {
+// #pragma unroll
+//   for (int i = 0; i < 8; ++i) *reinterpret_cast<bf16x8*>(buf + (C.w * 16 + H * 8 + i) * 1024 + C.lane * 16) = st[i];
+// }
+//
+// __device__ __forceinline__ uint32_t pack2(float a, float b) {
+//   typedef float f32x2_t __attribute__((ext_vector_type(2)));
+//   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2));
+// }
+//
+// template <bool BIAS>
+// __device__ __forceinline__ void w4r_epilogue(const f32x4 (&acc)[8][8], const char* bias_lds, bf16* __restrict__ c,
+//                                              int ldc, int m0, int n0, const W4Ctx& C) {
+//   const int ecol = (C.lq & 1) * 16 + (C.lq >> 1) * 8;
+//   bf16* base = c + (size_t)(m0 + C.wm * 128 + C.li) * ldc + n0 + C.wn * 128 + ecol;
+// #pragma unroll
+//   for (int nb = 0; nb < 8; nb += 2) {
+//     f32x4 bx = {0.f, 0.f, 0.f, 0.f}, by = {0.f, 0.f, 0.f, 0.f};
+//     if constexpr (BIAS) {
+//       bx = __builtin_convertvector(*reinterpret_cast<const bf16x4*>(bias_lds + (C.wn * 128 + nb * 16 + 4 * C.lq) * 2), f32x4);
+//       by = __builtin_convertvector(*reinterpret_cast<const bf16x4*>(bias_lds + (C.wn * 128 + (nb + 1) * 16 + 4 * C.lq) * 2), f32x4);
+//     }
+// #pragma unroll
+//     for (int mb = 0; mb < 8; ++mb) {
+//       const f32x4 X = acc[mb][nb] + bx, Y = acc[mb][nb + 1] + by;
+//       const uint32_t x0 = pack2(X[0], X[1]), x1 = pack2(X[2], X[3]);
+//       const uint32_t y0 = pack2(Y[0], Y[1]), y1 = pack2(Y[2], Y[3]);
+//       const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+//       const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+//       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+//       const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
+//       *reinterpret_cast<u32x4*>(base + (size_t)mb * 16 * ldc + nb * 16) = v;
+//     }
+//   }
+// }
+//
+// // fragments of one k-half: A[mb] (8) and B[nb] (8) of the wave's quarter
+// __device__ __forceinline__ void w4r_read(const char* buf, const W4Ctx& C, int kh, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+//   const char* pa = buf + C.abase + kh * C.kh1;
+//   const char* pb = buf + C.bbase + kh * C.kh1;
+// #pragma unroll
+//   for (int i = 0; i < 8; ++i) {
+//     fa[i] = *reinterpret_cast<const bf16x8*>(pa + i * 2048);
+//     fb[i] = *reinterpret_cast<const bf16x8*>(pb + i * 2048);
+//   }
+// }
+//
+// template <bool ZERO>
+// __device__ __forceinline__ void w4r_mfma(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
+// #pragma unroll
+//   for (int mb = 0; mb < 8; ++mb)
+// #pragma unroll
+//     for (int nb = 0; nb < 8; ++nb)
+//       acc[mb][nb] = mfma16(fb[nb], fa[mb], ZERO ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mb][nb]);
+// }
+//
+// // interleave per group: NDS LDS reads, NDW LDS writes, NVM VMEM loads, NMF MFMAs
+// #define DTD_W4R_SCHED(GROUPS, NDS, NDW, NVM, NMF)                            \
+//   do {                                                                       \
+//     _Pragma("unroll") for (int _g = 0; _g < (GROUPS); ++_g) {                \
+//       if ((NDS) > 0) __builtin_amdgcn_sched_group_barrier(0x100, (NDS), 0);  \
+//       if ((NDW) > 0) __builtin_amdgcn_sched_group_barrier(0x200, (NDW), 0);  \
+//       if ((NVM) > 0) __builtin_amdgcn_sched_group_barrier(0x020, (NVM), 0);  \
+//       __builtin_amdgcn_sched_group_barrier(0x008, (NMF), 0);                 \
+//     }                                                                        \
+//   } while (0)
+//
+// template <bool BIAS>
+// __global__ void __launch_bounds__(256, 1) gemm_bt_w4r(GemmArgs g) {
+//   __shared__ __attribute__((aligned(1024))) char smem[W4R_LDS];
+//   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+//   W4Ctx C;
+//   C.w = w; C.wm = w >> 1; C.wn = w & 1; C.li = lane & 15; C.lq = lane >> 4; C.lane = lane;
+//   const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn;
+//   const int nk = g.K / BK;   // >= 2 (host check)
+//   const int nwg = gridDim.x, x = blockIdx.x % 8, l = blockIdx.x / 8, per = nwg / 8;
+//   const int q = ntiles / 8, r = ntiles % 8;
+//   const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+//   const int end = beg + q + (x < r ? 1 : 0);
+//   int t = beg + l;
+//   if (t >= end) return;
+//   const int ntl = (end - t + per - 1) / per;   // tiles of this workgroup
+//   const int ng = ntl * nk;                     // its K-steps
+//   // staging: waves 0-1 carry A rows, 2-3 B rows; lane L -> row L/8 of an 8-row piece, chunk slot
+//   // L%8 <- global chunk (L%8) ^ (L/8) (the involutive swizzle of the fragment reads)
+//   const bool isb = w >= 2;
+//   const int ld = isb ? g.ldb : g.lda;
+//   C.voff = ((((w & 1) * 16 * 8) + (lane >> 3)) * ld + (((lane & 7) ^ (lane >> 3)) * 8)) * 2;
+//   const int sw = C.li & 7;
+//   C.abase = (C.wm * 128 + C.li) * 128 + ((C.lq ^ sw) * 16);
+//   C.bbase = A_BYTES + (C.wn * 128 + C.li) * 128 + ((C.lq ^ sw) * 16);
+//   C.kh1 = (((4 + C.lq) ^ sw) - (C.lq ^ sw)) * 16;
+//   auto panel = [&](int tile) {   // this wave's operand panel of `tile`
+//     int tm0, tn0;
+//     tile_of(tile, ntn, tm0, tn0);
+//     return uniform_rsrc(isb ? (const void*)(g.b + (size_t)tn0 * g.ldb) : (const void*)(g.a + (size_t)tm0 * g.lda));
+//   };
+//   const auto rbias = uniform_rsrc(BIAS ? (const void*)g.bias : (const void*)g.a);
+//   auto rs_cur = panel(t);
+//   auto rs_next = panel(t + per < end ? t + per : t);
+//   // source of global K-step gs + d relative to the tile of local step k (the next tile past nk)
+//   // staging ring of half a K-step (8 pieces): K-step s's half 0 is loaded in part 1 of K-step
+//   // s - 2 and stored in its part 2, half 1 loaded in part 2 of s - 2 and stored in part 1 of s - 1
+//   // (both into buffer s & 1, free from part 2 of s - 2 on, read from part 2 of s - 1 on)
+//   bf16x8 st[8];
+//   // prologue: K-steps 0 and 1 into the two buffers, K-step 2's first half in flight
+//   for (int kk = 0; kk < 2; ++kk)
+//     for (int H = 0; H < 2; ++H) {
+//       w4r_load(C, rs_cur, ld, kk, H, st);
+//       w4r_write(C, smem + kk * TILE_BYTES, H, st);
+//     }
+//   auto src = [&](int k, int d, int& kk) {   // panel and tile-local K-step of local step k + d
+//     const bool nxt = k + d >= nk;
+//     kk = nxt ? k + d - nk : k + d;
+//     return nxt ? rs_next : rs_cur;
+//   };
+//   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+//   bar();
+//   bf16x8 xa[8], xb[8], ya[8], yb[8];
+//   w4r_read(smem, C, 0, xa, xb);
+//   f32x4 acc[8][8];
+//   int m0, n0;
+//   tile_of(t, ntn, m0, n0);
+//   int it = 0;   // tile iteration of this workgroup
+//   // One K-step, branch-free (one basic block, so the sched_group_barrier interleave applies):
+//   // past the workgroup's last K-steps the loads re-read a valid panel and the stores / reads touch
+//   // buffers nobody consumes any more; the first K-step after the prologue re-stores the prologue's
+//   // last half (identical bytes).
+//   int gs = 0;
+//   auto kstep = [&](auto first_c, int k) {
+//     constexpr bool first = decltype(first_c)::value;
+//     char* cur = smem + (gs & 1) * TILE_BYTES;
+//     char* oth = smem + ((gs & 1) ^ 1) * TILE_BYTES;
+//     int kk;
+//     const auto rs2 = src(k, 2, kk);
+//     // ---- part 1: k-half 0 MFMAs (X) | k-half 1 reads (Y) | K-step gs + 1's second half stored
+//     //      (into `oth`, read from part 2 on) | K-step gs + 2's first half loaded
+//     w4r_read(cur, C, 1, ya, yb);
+//     w4r_write(C, oth, 1, st);
+//     w4r_load(C, rs2, ld, kk, 0, st);
+//     w4r_mfma<first>(acc, xa, xb);
+//     DTD_W4R_SCHED(8, 2, 1, 1, 8);
+//     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Y in registers, the stores done
+//     bar();
+//     // ---- part 2: k-half 1 MFMAs (Y) | k-half 0 reads of K-step gs + 1 (X) | K-step gs + 2's
+//     //      first half stored into `cur` (read out in part 1), its second half loaded
+//     w4r_read(oth, C, 0, xa, xb);
+//     if constexpr (BIAS && first) {   // this tile's bias -> its LDS slot (waves 0-1), read in its epilogue
+//       __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias, (lds_void*)(smem + LDS_BYTES + (it & 1) * 512 + (w & 1) * 256),
+//                                                 4, (n0 + (w & 1) * 128) * 2 + lane * 4, 0, 0, 0);
+//     }
+//     w4r_write(C, cur, 0, st);
+//     w4r_load(C, rs2, ld, kk, 1, st);
+//     w4r_mfma<false>(acc, ya, yb);
+//     DTD_W4R_SCHED(8, 2, 1, 1, 8);
+//     ++gs;
+//   };
+//   for (int gs0 = 0; gs0 < ng; gs0 += nk) {   // one tile
+//     kstep(std::true_type{}, 0);
+//     for (int k = 1; k < nk; ++k) kstep(std::false_type{}, k);
+//     // ---- tile done: epilogue, then the next tile
+//     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the bias LDS-DMA (waves 0-1)
+//     bar();
+//     w4r_epilogue<BIAS>(acc, smem + LDS_BYTES + (it & 1) * 512, g.c, g.ldc, m0, n0, C);
+//     ++it;
+//     t += per;
+//     tile_of(t < end ? t : beg, ntn, m0, n0);
+//     rs_cur = rs_next;
+//     rs_next = panel(t + per < end ? t + per : t);
+//   }
+// }
