@@ -108,3 +108,24 @@ def test_zero_script_graph_trains_like_eager(stage):
         res[mode] = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert res["on"]["hip_graph"] and not res["off"]["hip_graph"]
     assert res["on"]["final_loss"] == res["off"]["final_loss"]
+
+
+def test_zero_script_graph_captures_bert_mlm_head():
+    """zero_dp_training.py with a BERT model at world size 1 captures the step as a hipGraph: the
+    sparse MLM head's labelled-row gather gets a static size (the script's causal-LM data labels
+    every position) instead of a host-synchronising nonzero()."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(32000 + os.getpid() % 1000))
+    r = subprocess.run([sys.executable, os.path.join(root, "zero_dp_training.py"), "--model-name", "bert-tiny",
+                        "--stage", "2", "--batch-size", "2", "--training-steps", "8", "--seq-len", "128", "--quiet",
+                        "--no-memstats"], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{") and "tokens_per_s" in ln][-1]
+    d = json.loads(line)
+    assert d["hip_graph"] is True and d["stage"] == 2
+    assert d["final_loss"] == d["final_loss"]   # finite (not NaN)

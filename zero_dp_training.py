@@ -87,6 +87,11 @@ def train(model_name, batch_size, training_steps, stage, opts):
         # Captured before the clock starts (3 eager warm-up steps on the first batch, like
         # data_parallel_training.py --graph)
         from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep
+        rt = getattr(model, "rt", None)
+        if rt is not None and cfg.family == "bert":
+            # the sparse MLM head gathers its labelled rows; the causal-LM data here (mlm=False)
+            # labels every position, so a static gather of all of them keeps the step capturable
+            rt.mlm_capacity = batch_size * opts.seq_len
         warm = [b for _, b in zip(range(min(3, training_steps)), batches)]
         graphed = None if not warm else CapturedStep(train_step, warm[0], warmup_batches=warm, runtime=getattr(model, "rt", None))
         loss = graphed.warmup_losses[-1] if graphed is not None else None
@@ -146,8 +151,8 @@ if __name__ == "__main__":
     parser.add_argument("--num-gpus", type=int, default=None, help="spawn locally (like `deepspeed --num_gpus`)")
     parser.add_argument("--no-memstats", action="store_true")
     parser.add_argument("--graph", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
-                        help="stages 0/1: capture the whole training step in a hipGraph and replay it "
-                             "(auto: on for one GPU at stage 0/1, where batch-1 steps are host-launch bound)")
+                        help="capture the whole training step in a hipGraph and replay it, at any ZeRO stage "
+                             "(auto: on for one GPU, where batch-1 steps are host-launch bound)")
     parser.add_argument("--quiet", action="store_true")
     args, extra_args = parser.parse_known_args()
     if args.num_gpus and "WORLD_SIZE" not in os.environ:
