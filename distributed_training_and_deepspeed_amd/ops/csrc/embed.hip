@@ -9,6 +9,7 @@
 // token ids are sorted once (on device), and each run of equal ids is summed in fp32 by one
 // workgroup that owns that table row exclusively, so there are no float atomics and the
 // result is bitwise reproducible (cdna_hip_programming.md Appendix B "Scatter / gather").
+#include <algorithm>
 #include "common.h"
 
 using namespace dtd;
@@ -85,6 +86,7 @@ __global__ void __launch_bounds__(256) embed_word_bwd_kernel(const int64_t* __re
 // per chunk), pass 2 adds a segment's chunk sums in order into the table row.  seg_lo/seg_hi
 // are the [first, last+1) sorted positions of each position's id (searchsorted left/right).
 constexpr int kChunk = 16;
+constexpr int kUnroll = 8;   // rows (chunk sums) loaded ahead per step of the serial sums below
 // Chunk length of a segment: at least kChunk, and ~sqrt(len) for long ones, so neither pass
 // sums more than ~sqrt(len) rows serially in one wave (synthetic MLM batches hold one [MASK]
 // segment of ~12 % of all tokens: 7.9k rows at b128, 492 serial partial rows with fixed chunks).
@@ -102,23 +104,39 @@ __global__ void __launch_bounds__(256) embed_chunk_sum_kernel(const int64_t* __r
                                                               const int64_t* __restrict__ seg_hi,
                                                               const T* __restrict__ dz, float* __restrict__ scratch,
                                                               int rows, int h) {
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (i >= rows) return;
+  const int lane = threadIdx.x & 63;
+  // grid-stride over sorted positions (one wave each): a grid of one wave per position spent its
+  // time dispatching the waves of non-leader positions, which exit at once
+  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < rows; i += gridDim.x * 4) {
   const int lo = (int)seg_lo[i], shi = (int)seg_hi[i];
   const int ch = chunk_len(shi - lo);
-  if ((i - lo) % ch) return;
+  if ((i - lo) % ch) continue;
   const int end = min(i + ch, shi);
   for (int c = lane * VEC; c < h; c += 64 * VEC) {
     float acc[VEC];
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
-    for (int k = i; k < end; ++k) {
+    // kUnroll rows' loads in flight at once, summed in row order (the same result as one row at
+    // a time): a chunk of a long segment is ~sqrt(len) rows, and one dependent HBM round trip per
+    // row made the longest chunk the kernel's critical path
+    int k = i;
+    for (; k + kUnroll <= end; k += kUnroll) {
+      float x[kUnroll][VEC];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) vload<T, VEC>(dz + (size_t)perm[k + u] * h + c, x[u]);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] += x[u][j];
+    }
+    for (; k < end; ++k) {
       float x[VEC];
       vload<T, VEC>(dz + (size_t)perm[k] * h + c, x);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) acc[j] += x[j];
     }
     vstore<float, VEC>(scratch + (size_t)i * h + c, acc);
+  }
   }
 }
 
@@ -128,10 +146,11 @@ __global__ void __launch_bounds__(256) embed_chunk_add_kernel(const int64_t* __r
                                                               const int64_t* __restrict__ seg_hi,
                                                               const float* __restrict__ scratch, G* __restrict__ grad,
                                                               int rows, int h, int accumulate, int padding_idx) {
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (i >= rows || seg_lo[i] != i) return;
+  const int lane = threadIdx.x & 63;
+  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < rows; i += gridDim.x * 4) {   // grid-stride, as above
+  if (seg_lo[i] != i) continue;
   const int64_t id = sorted_ids[i];
-  if (id == padding_idx) return;
+  if (id == padding_idx) continue;
   const int hi = (int)seg_hi[i];
   const int ch = chunk_len(hi - i);
   G* g = grad + (size_t)id * h;
@@ -139,7 +158,17 @@ __global__ void __launch_bounds__(256) embed_chunk_add_kernel(const int64_t* __r
     float acc[VEC];
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
-    for (int k = i; k < hi; k += ch) {
+    int k = i;
+    for (; k + kUnroll * ch <= hi; k += kUnroll * ch) {   // kUnroll chunk sums in flight, added in order
+      float x[kUnroll][VEC];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) vload<float, VEC>(scratch + (size_t)(k + u * ch) * h + c, x[u]);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] += x[u][j];
+    }
+    for (; k < hi; k += ch) {
       float x[VEC];
       vload<float, VEC>(scratch + (size_t)k * h + c, x);
 #pragma unroll
@@ -152,6 +181,7 @@ __global__ void __launch_bounds__(256) embed_chunk_add_kernel(const int64_t* __r
       for (int j = 0; j < VEC; ++j) acc[j] += old[j];
     }
     vstore<G, VEC>(g + c, acc);
+  }
   }
 }
 
@@ -299,7 +329,7 @@ DTD_EXPORT int dtd_embed_word_bwd_chunked(int dtype, int grad_dtype, const int64
                                           const int64_t* seg_lo, const int64_t* seg_hi, float* scratch, const void* dz,
                                           void* grad, int rows, int h, int accumulate, int padding_idx, hipStream_t s) {
   if (rows <= 0) return 0;
-  const dim3 grid((rows + 3) / 4);
+  const dim3 grid(std::min((rows + 3) / 4, 256 * 6));   // grid-stride kernels: one round of waves
 #define DTD_EMB_LAUNCH(V)                                                                                      \
   if (dtype == kBF16)                                                                                          \
     hipLaunchKernelGGL((embed_chunk_sum_kernel<bf16, V>), grid, dim3(256), 0, s, perm, seg_lo, seg_hi,         \

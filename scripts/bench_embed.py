@@ -24,7 +24,8 @@ def t_us(fn, reps=20):
 
 
 def main():
-    T, V, h = 65536, 28996, 768
+    T, V, h = int(os.environ.get("T", 65536)), 28996, 768
+    torch.manual_seed(0)
     ids = torch.randint(0, V, (T,), device="cuda")
     if os.environ.get("SKEW", "1") == "1":   # synthetic MLM batches: ~12 % of tokens are [MASK]
         ids[torch.rand(T, device="cuda") < 0.12] = 103
@@ -32,12 +33,15 @@ def main():
     g = torch.zeros(V, h, device="cuda", dtype=torch.bfloat16)
     r = {}
     r["word_bwd_total"] = t_us(lambda: Fx.embed_word_bwd(ids, dz, g, False, padding_idx=0))
+    Fx.embed_word_bwd(ids, dz, g, False, padding_idx=0)
+    gi = g.view(torch.int16).to(torch.int64)
+    r["checksum"] = int((gi * torch.arange(1, gi.numel() + 1, device="cuda").view_as(gi) % 1000003).sum().item())
     r["sort"] = t_us(lambda: torch.sort(ids, stable=True))
     s, perm = torch.sort(ids, stable=True)
     r["searchsorted_x2"] = t_us(lambda: (torch.searchsorted(s, s, right=False), torch.searchsorted(s, s, right=True)))
     r["zero_"] = t_us(lambda: g.zero_())
     r["scratch_alloc"] = t_us(lambda: torch.empty((T, h), dtype=torch.float32, device="cuda"))
-    print(json.dumps({k: round(v, 1) for k, v in r.items()}))
+    print(json.dumps({"T": T, **{k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}}))
 
 
 if __name__ == "__main__":
