@@ -18,7 +18,7 @@ from torch import nn
 
 from .config import BERT_BASE, TransformerConfig, get_config
 from .layers import Embeddings, MLMHead
-from .transformer import Runtime, TransformerLayer, prefetch_masks
+from .transformer import Runtime, TransformerLayer, prefetch_masks, stage_dgrad_transposes
 
 
 @dataclass
@@ -54,6 +54,7 @@ class BertForMaskedLM(nn.Module):
         x = self.embeddings(input_ids)
         for layer in self.layers:
             x = layer(x)
+        stage_dgrad_transposes(self.layers, x)
         return x
 
     def forward(self, input_ids: torch.Tensor, labels: torch.Tensor | None = None,

@@ -19,7 +19,7 @@ from torch import nn
 
 from .config import BLOOM_560M, TransformerConfig, get_config
 from .layers import Embeddings, LayerNorm, LMHead
-from .transformer import Runtime, TransformerLayer, prefetch_masks
+from .transformer import Runtime, TransformerLayer, prefetch_masks, stage_dgrad_transposes
 
 
 @dataclass
@@ -56,6 +56,7 @@ class CausalLM(nn.Module):
         x = self.embeddings(input_ids)
         for layer in self.layers:
             x = layer(x)
+        stage_dgrad_transposes(self.layers, x)
         if self.final_ln is not None:
             x = self.final_ln(x)
         return x

@@ -58,6 +58,7 @@ class Runtime:
         # its rewrite: the backward pass then moves 3 instead of 4 T x ffn tensors through HBM.
         # Memory-bound runs (max-params ZeRO-3) turn it off.
         self.keep_ffn_act = True
+        self.pending_wt: list | None = None   # weights to batch-transpose at the start of the backward
 
     def new_sid(self) -> int:
         """Dropout stream id for one call site; deterministic per model structure so two
@@ -72,6 +73,19 @@ class Runtime:
         if self.impl == "reference":
             return False
         return x.is_cuda
+
+
+def stage_dgrad_transposes(layers, x: torch.Tensor) -> None:
+    """End of a forward: drop the previous backward's W^T copies, and for a training forward on the
+    fused path let the first layer backward transpose every layer's NT input-gradient operands in
+    one batched launch (ops/gemm.py::prepare_transposes)."""
+    G.clear_transposes()
+    if not layers:
+        return
+    rt = layers[0].rt
+    rt.pending_wt = None
+    if layers[0].training and torch.is_grad_enabled() and x.is_cuda and rt.use_fused(x):
+        rt.pending_wt = [w for layer in layers for w in (layer.qkv_w, layer.o_w, layer.fc1_w, layer.fc2_w)]
 
 
 def prefetch_masks(layers, input_ids: torch.Tensor) -> None:
@@ -297,6 +311,9 @@ class _FusedLayerFn(torch.autograd.Function):
         B, S, h, H, D, p_h, p_a, sa, s1, s2 = ctx.meta
         T = B * S
         (qkv_w, qkv_b, o_w, o_b, g1, b1, w1, bf1, w2, bf2, g2, b2) = layer.params()
+        pend, layer.rt.pending_wt = layer.rt.pending_wt, None
+        if pend:   # first layer backward of the step: every layer's W^T in one launch
+            G.prepare_transposes(pend)
         dout = dout.reshape(T, h).contiguous()
         if c.pre_ln:
             x2d, a_in, qkv, actx, lse, z1, f_in, u, m1, r1, m2, r2, a = ctx.saved_tensors
@@ -317,7 +334,7 @@ class _FusedLayerFn(torch.autograd.Function):
         w2t = None
         if (a is not None and G.ffn_bwd_enabled() and c.activation in G.FUSED_ACTS and dy.is_cuda
                 and dy.dtype == torch.bfloat16 and G.supported(dy.shape[0], w2.shape[1], dy.shape[1], dy, u)):
-            w2t = G.transpose(w2)                      # [ffn, hidden]: K-contiguous B operand
+            w2t = G.transposed(w2)                     # [ffn, hidden]: K-contiguous B operand
         if ctx.ffn_g:
             # u holds act'(u): dU = dA * u
             if w2t is not None:

@@ -1039,10 +1039,10 @@ __global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16* __restr
   }
 }
 
-__global__ void __launch_bounds__(256) transpose_bf16_vec_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
-                                                                 int rows, int cols) {
+// one 64 x 64 tile (rows r0.., columns c0..) of the vector form
+__device__ __forceinline__ void transpose_tile_vec(const bf16* __restrict__ in, bf16* __restrict__ out, int rows,
+                                                   int cols, int r0, int c0) {
   __shared__ bf16 tile[64][72];
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int t = threadIdx.x, cv = (t & 7) * 8, rv = t >> 3;   // 8 vectors per 64-wide row
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -1064,6 +1064,30 @@ __global__ void __launch_bounds__(256) transpose_bf16_vec_kernel(const bf16* __r
       *reinterpret_cast<bf16x8*>(out + (size_t)(c0 + cc) * rows + r0 + cv) = v;
     }
   }
+}
+
+__global__ void __launch_bounds__(256) transpose_bf16_vec_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
+                                                                 int rows, int cols) {
+  transpose_tile_vec(in, out, rows, cols, blockIdx.y * 64, blockIdx.x * 64);
+}
+
+// Many weights transposed in one launch (the NT input-gradient operands of a whole model at the
+// start of its backward, instead of one small launch per weight per layer): workgroup b takes
+// tile b - tile0[e] of entry e, tile0 the entries' running tile counts (kernel-argument arrays,
+// indexed wave-uniformly).
+constexpr int kMaxTranspose = 64;
+struct TransposeSet {
+  const bf16* in[kMaxTranspose];
+  bf16* out[kMaxTranspose];
+  int rows[kMaxTranspose], cols[kMaxTranspose], tile0[kMaxTranspose + 1];
+  int n;
+};
+__global__ void __launch_bounds__(256) transpose_many_kernel(TransposeSet s) {
+  const int b = blockIdx.x;
+  int e = 0;
+  while (e + 1 < s.n && s.tile0[e + 1] <= b) ++e;
+  const int ntc = (s.cols[e] + 63) / 64, t = b - s.tile0[e];
+  transpose_tile_vec(s.in[e], s.out[e], s.rows[e], s.cols[e], (t / ntc) * 64, (t % ntc) * 64);
 }
 
 }  // namespace
@@ -1214,6 +1238,30 @@ DTD_EXPORT int dtd_gemm_tn(const void* a, int lda, const void* b, int ldb, float
   TnArgs g{(const bf16*)a, (const bf16*)b, part, M, N, K, lda, ldb, splits, ksplit};
   const int ntiles = (M / BM) * (N / BN);
   hipLaunchKernelGGL(gemm_tn_kernel, dim3(ntiles * splits), dim3(512), 0, s, g);
+  DTD_LAUNCH_CHECK();
+}
+
+// ins[i] [rows[i]][cols[i]] -> outs[i] [cols[i]][rows[i]] for i < n in one launch (vector form only:
+// rows, cols multiples of 8, 16-byte aligned pointers; n <= 64)
+DTD_EXPORT int dtd_transpose_many(const void* const* ins, void* const* outs, const int* rows, const int* cols, int n,
+                                  hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n > kMaxTranspose) return (int)hipErrorInvalidValue;
+  TransposeSet set{};
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    if (rows[i] <= 0 || cols[i] <= 0 || rows[i] % 8 || cols[i] % 8 || ((uintptr_t)ins[i] | (uintptr_t)outs[i]) % 16)
+      return (int)hipErrorInvalidValue;
+    set.in[i] = (const bf16*)ins[i];
+    set.out[i] = (bf16*)outs[i];
+    set.rows[i] = rows[i];
+    set.cols[i] = cols[i];
+    set.tile0[i] = tiles;
+    tiles += ((rows[i] + 63) / 64) * ((cols[i] + 63) / 64);
+  }
+  set.tile0[n] = tiles;
+  set.n = n;
+  hipLaunchKernelGGL(transpose_many_kernel, dim3(tiles), dim3(256), 0, s, set);
   DTD_LAUNCH_CHECK();
 }
 

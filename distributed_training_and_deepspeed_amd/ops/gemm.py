@@ -26,6 +26,7 @@ the elementwise kernels otherwise.  bf16 only.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -251,6 +252,54 @@ def transposed_for_dgrad(w: torch.Tensor) -> torch.Tensor | None:
         return None
     if w.shape[0] % 8:   # W^T rows (the GEMM's K) would not be 16-byte aligned (e.g. a 28996-row vocabulary)
         return None
+    return transposed(w)
+
+
+# W^T of the weights of one backward, made by ONE batched launch at its start
+# (prepare_transposes) instead of one small launch per weight as each layer's backward reaches it
+# (49 launches of ~6 us at BERT-base).  Keyed by the parameter object and checked against its
+# current storage address; cleared at the start of every forward (the weights change only at the
+# optimizer step, which precedes the next forward).
+_WT_CACHE: dict = {}
+_WT_BATCH = [os.environ.get("DTD_WT_BATCH", "1") == "1"]
+
+
+def clear_transposes() -> None:
+    _WT_CACHE.clear()
+
+
+def _batchable(w: torch.Tensor, dev) -> bool:
+    return (w.is_cuda and w.device == dev and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()
+            and w.numel() > 0 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and w.data_ptr() % 16 == 0)
+
+
+def prepare_transposes(weights) -> None:
+    """Transpose every eligible weight of ``weights`` (resident, on the current device) in batched
+    launches of up to 64; transposed() then returns the cached copies."""
+    if not (_WT_BATCH[0] and _lib.has("dtd_transpose_many")):
+        return
+    if any(w.numel() == 0 for w in weights):
+        return   # partitioned parameters (ZeRO-3 releases them between uses): per-call transposes
+    dev = torch.device("cuda", torch.cuda.current_device())
+    todo = [w for w in weights if _batchable(w, dev) and id(w) not in _WT_CACHE]
+    for k in range(0, len(todo), 64):
+        chunk = todo[k:k + 64]
+        outs = [torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device) for w in chunk]
+        n = len(chunk)
+        ins_a = (ctypes.c_void_p * n)(*[w.data_ptr() for w in chunk])
+        outs_a = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+        rows_a = (ctypes.c_int * n)(*[w.shape[0] for w in chunk])
+        cols_a = (ctypes.c_int * n)(*[w.shape[1] for w in chunk])
+        _lib.call("dtd_transpose_many", ins_a, outs_a, rows_a, cols_a, n, _lib.stream())
+        for w, o in zip(chunk, outs):
+            _WT_CACHE[id(w)] = (w, w.data_ptr(), o)
+
+
+def transposed(w: torch.Tensor) -> torch.Tensor:
+    """W^T: the copy prepare_transposes made for this backward, else a fresh transpose."""
+    e = _WT_CACHE.get(id(w))
+    if e is not None and e[0] is w and e[1] == w.data_ptr():
+        return e[2]
     return transpose(w)
 
 
