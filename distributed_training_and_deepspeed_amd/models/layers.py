@@ -295,7 +295,7 @@ class MLMHead(nn.Module):
         cap = self.rt.mlm_capacity
         if cap is None:
             idx = valid.nonzero().squeeze(1)
-            return x2.index_select(0, idx), lab.index_select(0, idx)
+            return _gather_rows(x2, idx, None, idx.numel()), lab.index_select(0, idx)
         cap = min(cap, lab.numel())
         idx = torch.nonzero_static(valid, size=cap, fill_value=0).squeeze(1)
         count = valid.sum()
@@ -303,7 +303,7 @@ class MLMHead(nn.Module):
         lab_sel = torch.where(keep, lab.index_select(0, idx), torch.full_like(idx, Fx.IGNORE_INDEX))
         if self.rt.mlm_overflow is not None:
             self.rt.mlm_overflow.logical_or_(count > cap)
-        return x2.index_select(0, idx), lab_sel
+        return _gather_rows(x2, idx, count, cap), lab_sel
 
     def loss(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         h = self.cfg.hidden_size
@@ -316,6 +316,34 @@ class MLMHead(nn.Module):
             return _MLMHeadFn.apply(x2, lab, self, *self.params())
         logits = self.logits(x2)
         return F.cross_entropy(logits.float(), lab, ignore_index=Fx.IGNORE_INDEX)
+
+
+class _GatherRows(torch.autograd.Function):
+    """x[idx] whose backward writes the whole [rows, h] input gradient in one kernel pass
+    (ops/csrc/embed.hip scatter_rows_kernel: labelled rows copied, the rest zero) instead of a zero
+    fill plus index_add.  idx[0:n) ascending and unique, n = min(count, cap); entries past n are
+    static-capacity padding whose gradient rows are zero (label -100)."""
+
+    @staticmethod
+    def forward(ctx, x, idx, count, cap):
+        ctx.rows, ctx.cap, ctx.has_count = x.shape[0], int(cap), count is not None
+        ctx.save_for_backward(idx, count if count is not None else idx)
+        return x.index_select(0, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, count = ctx.saved_tensors
+        g = g.contiguous()
+        return Fx.scatter_rows(g, idx, count if ctx.has_count else None, ctx.cap, ctx.rows), None, None, None
+
+
+_SCATTER_ROWS = [os.environ.get("DTD_MLM_SCATTER", "1") == "1"]
+
+
+def _gather_rows(x: torch.Tensor, idx: torch.Tensor, count, cap: int) -> torch.Tensor:
+    if _SCATTER_ROWS[0] and Fx.scatter_rows_supported(x) and torch.is_grad_enabled() and x.requires_grad:
+        return _GatherRows.apply(x, idx, count, cap)
+    return x.index_select(0, idx)
 
 
 # ----------------------------------------------------------------------------- causal LM head

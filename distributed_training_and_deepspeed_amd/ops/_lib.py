@@ -53,6 +53,7 @@ _SIGS = {
     "dtd_embed_fwd": (I, [I, P, P, P, P, P, P, I, I, I, I, P]),
     "dtd_embed_word_bwd": (I, [I, I, P, P, P, P, I, I, I, I, P]),
     "dtd_embed_pos_bwd": (I, [I, I, P, P, I, I, I, I, I, P]),
+    "dtd_scatter_rows": (I, [P, P, P, I, P, I, I, P]),
     "dtd_dropout": (I, [I, P, P, P, SZ, F, P, U32, P]),
     "dtd_embed_ln_fwd": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, F, F, P, U32, P]),
     # adam.hip

@@ -223,6 +223,38 @@ __global__ void __launch_bounds__(256) embed_pos_bwd_kernel(const T* __restrict_
   }
 }
 
+// Backward of a row gather (the sparse MLM head's labelled rows, models/layers.py::_GatherRows):
+// out[r] = g[p] where idx[p] == r for p < n (idx[0:n) ascending, unique), else 0 -- one pass that
+// writes every row once, instead of a zero fill plus an index_add.  n = min(*count, cap) when a
+// device count is given (static-capacity gather: entries past the count are padding), else cap.
+template <int VEC>
+__global__ void __launch_bounds__(256) scatter_rows_kernel(const bf16* __restrict__ g, const int64_t* __restrict__ idx,
+                                                           const int64_t* __restrict__ count, int cap,
+                                                           bf16* __restrict__ out, int rows, int h) {
+  const int lane = threadIdx.x & 63;
+  const int n = count ? (int)min((int64_t)cap, *count) : cap;
+  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += gridDim.x * 4) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (idx[mid] < r) lo = mid + 1;
+      else hi = mid;
+    }
+    const bool hit = lo < n && idx[lo] == r;
+    bf16* o = out + (size_t)r * h;
+    for (int c = lane * VEC; c < h; c += 64 * VEC) {
+      float v[VEC];
+      if (hit) {
+        vload<bf16, VEC>(g + (size_t)lo * h + c, v);
+      } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) v[j] = 0.f;
+      }
+      vstore<bf16, VEC>(o + c, v);
+    }
+  }
+}
+
 template <typename T>
 // y = dropout(x), or y = res + dropout(x) with the sum in fp32 (pre-LN residual branch: one pass
 // instead of a dropout pass + an add pass)
@@ -260,6 +292,15 @@ __global__ void __launch_bounds__(256) dropout_kernel(const T* __restrict__ x, c
 }
 
 }  // namespace
+
+DTD_EXPORT int dtd_scatter_rows(const void* g, const int64_t* idx, const int64_t* count, int cap, void* out, int rows,
+                                int h, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (h % 8 || ((uintptr_t)g | (uintptr_t)out) % 16) return (int)hipErrorInvalidValue;
+  const dim3 grid(std::min((rows + 3) / 4, 256 * 8));
+  hipLaunchKernelGGL(scatter_rows_kernel<8>, grid, dim3(256), 0, s, (const bf16*)g, idx, count, cap, (bf16*)out, rows, h);
+  DTD_LAUNCH_CHECK();
+}
 
 DTD_EXPORT int dtd_embed_fwd(int dtype, const int64_t* ids, const int64_t* type_ids, const void* word, const void* pos,
                              const void* type, void* out, int rows, int h, int seq, int pos_offset, hipStream_t s) {

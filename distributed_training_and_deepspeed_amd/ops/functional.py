@@ -466,6 +466,21 @@ def embed_ln_fwd(ids, word, pos, type_, seq: int, pos_offset: int, gamma, beta, 
     return out, z, mean, rstd
 
 
+def scatter_rows_supported(g: torch.Tensor) -> bool:
+    return (g.is_cuda and g.dtype == torch.bfloat16 and g.dim() == 2 and g.is_contiguous() and g.shape[1] % 8 == 0
+            and g.data_ptr() % 16 == 0 and _lib.has("dtd_scatter_rows"))
+
+
+def scatter_rows(g: torch.Tensor, idx: torch.Tensor, count: torch.Tensor | None, cap: int, rows: int) -> torch.Tensor:
+    """[rows, h] with row idx[p] = g[p] for p < n and zeros elsewhere, n = min(count, cap) (count: a
+    device scalar, None -> cap); idx[0:n) ascending and unique (the backward of a row gather)."""
+    out = torch.empty((rows, g.shape[1]), dtype=g.dtype, device=g.device)
+    assert idx.dtype == torch.int64 and idx.is_contiguous() and cap <= idx.numel() and cap <= g.shape[0]
+    _lib.call("dtd_scatter_rows", g.data_ptr(), idx.data_ptr(), _lib.ptr(count), int(cap), out.data_ptr(), rows,
+              g.shape[1], _lib.stream())
+    return out
+
+
 def embed_word_bwd(ids: torch.Tensor, dz: torch.Tensor, grad: torch.Tensor, acc: bool, padding_idx: int = -1):
     flat = ids.reshape(-1)
     h = grad.shape[1]

@@ -87,7 +87,7 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "no_gemm": _env(DTD_GEMM="0"), "gemm_bwd_only": _env(DTD_GEMM_FFN_FWD="0"),
            "gemm_fwd_only": _env(DTD_GEMM_FFN_BWD="0"), "gemm_tile": _env(DTD_GEMM_VARIANT="0"),
            "no_gemm_wgrad": _env(DTD_GEMM_WGRAD="0"), "gemm_wgrad": _env(DTD_GEMM_WGRAD="1"),
-           "mask_ballot": _env(DTD_ATTN_MASK="0"), "wt_batch_off": _env(DTD_WT_BATCH="0"), "no_qkv_bias_fused": _env(DTD_ATTN_QKV_BIAS="0"),
+           "mask_ballot": _env(DTD_ATTN_MASK="0"), "mlm_scatter_off": _env(DTD_MLM_SCATTER="0"), "wt_batch_off": _env(DTD_WT_BATCH="0"), "no_qkv_bias_fused": _env(DTD_ATTN_QKV_BIAS="0"),
            "no_ffn_store_grad": _env(DTD_GEMM_FFN_STORE_GRAD="0"),
            "opt_overlap_off": lambda: ["--opt-overlap", "off"], "gemm_sched_static": _env(DTD_GEMM_SCHED="static"),
            "no_fused_embed_ln": _env(DTD_FUSED_EMBED_LN="0"), "no_fused_xent": _env(DTD_FUSED_XENT="0"), "fused_xent": _env(DTD_FUSED_XENT="1"), "no_defer_finalize": _env(DTD_DEFER_FINALIZE="0"),
