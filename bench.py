@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--opt-overlap", default=os.environ.get("DTD_OPT_OVERLAP", "on"), choices=["on", "off"],
                     help="DDP: the Adam update runs stage by stage on a side stream and the next forward "
                          "waits per stage (FusedAdam.overlap_with_forward; bit-identical results)")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="issue the DDP bucket all-reduces / ZeRO reduce-scatters and all-gathers through RCCL "
+                         "even at world size 1 (the N > 1 data path on one GPU)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
     return ap.parse_args()
@@ -92,7 +95,7 @@ def main():
             from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
             tuned = use_tuned_gemms()
     device = torch.device("cuda", local) if cuda else torch.device("cpu")
-    if world > 1 or args.zero_stage is not None:   # the ZeRO engine always runs on a process group
+    if world > 1 or args.zero_stage is not None or args.force_collectives:   # ZeRO always runs on a group
         comm.init(rank=rank, world_size=world, local_rank=local)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     cfg = get_config(args.model)
@@ -112,14 +115,16 @@ def main():
                 "optimizer": {"type": "Adam", "params": {"lr": 1.5e-4}},
                 # the partitioned data flow even at world 1 (the path every rank runs at N > 1)
                 "zero_optimization": {"stage": args.zero_stage, "reduce_bucket_size": args.reduce_bucket,
-                                      "world1_replicated": False},
+                                      "world1_replicated": False,
+                                      "force_collectives": args.force_collectives},
                 "bf16": {"enabled": dtype == torch.bfloat16}}
         engine, _, _, _ = initialize(model=model, model_parameters=model.parameters(), config=zcfg)
         gdt = engine.grad_dtype
     else:
         ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt,
                                       small_bucket_allreduce=args.small_bucket_allreduce,
-                                      async_wgrad=args.async_wgrad == "on")
+                                      async_wgrad=args.async_wgrad == "on",
+                                      force_collectives=args.force_collectives)
         opt = hf_adamw(ddp.parameters(), lr=5e-5)
 
     B, S = args.batch_size, args.seq_len
@@ -225,6 +230,7 @@ def main():
                               else "fused AdamW (transformers.AdamW hyper-params, lr 5e-5)"),
                 "tuned_gemms": tuned,
                 "hip_graph": graphed is not None,
+                "force_collectives": args.force_collectives,
                 "async_wgrad": args.async_wgrad == "on",
                 "opt_overlap": opt_overlap,
                 "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if cuda else None,
@@ -233,7 +239,7 @@ def main():
             "loss_last": round(float(loss.detach()), 4),
         }
         print(json.dumps(res), flush=True)
-    if world > 1 or zero:
+    if world > 1 or zero or args.force_collectives:
         comm.destroy()
 
 

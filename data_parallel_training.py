@@ -46,7 +46,8 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
     model.train()
     model.rt.rng.reseed(rank)   # independent dropout masks per replica (parameters are broadcast)
     ddp = DistributedDataParallel(model, bucket_cap_mb=bucket_size,
-                                  grad_dtype={"bf16": torch.bfloat16, "fp32": torch.float32}.get(opts.grad_dtype, dtype))
+                                  grad_dtype={"bf16": torch.bfloat16, "fp32": torch.float32}.get(opts.grad_dtype, dtype),
+                                  force_collectives=opts.force_collectives)
     optimizer = hf_adamw(ddp.parameters(), lr=5e-5)
     if opts.resume:
         meta = load_checkpoint(opts.resume, model, optimizer)
@@ -139,6 +140,8 @@ if __name__ == "__main__":
     parser.add_argument("--backend", default=None, choices=[None, "nccl", "gloo"])
     parser.add_argument("--impl", default="auto", choices=["auto", "fused", "reference"])
     parser.add_argument("--quiet", action="store_true")
+    parser.add_argument("--force-collectives", action="store_true",
+                        help="bucket all-reduces through RCCL even on one GPU (the N > 1 data path)")
     parser.add_argument("--metrics-json", default="", help="write tokens/s, step-time percentiles, peak HBM here")
     parser.add_argument("--markers", action="store_true", help="roctx ranges per phase (rocprofv3 --marker-trace)")
     parser.add_argument("--save-dir", default="", help="write <dir>/ddp_checkpoint.pt at the end")

@@ -79,6 +79,9 @@ _SIGS = {
     "dtd_gemm_tn_supported": (I, [I, I, I]),
     "dtd_gemm_tn_splits": (I, [I, I, I]),
     "dtd_gemm_tn": (I, [P, I, P, I, P, I, I, I, I, P]),
+    # gemm4.hip
+    "dtd_gemm4_supported": (I, [I, I, I]),
+    "dtd_gemm4_bt": (I, [I, P, I, P, I, P, I, P, I, I, I, P]),
     # reduce.hip
     "dtd_splitk_reduce": (I, [P, I, I, ctypes.c_longlong, P, I, I, P]),
 }

@@ -25,6 +25,10 @@ reducer:
 * Optional native path for small buckets (``small_bucket_allreduce="xgmi"``): buckets of at
   most ``xgmi_max_mb`` go through the peer-mapped one-shot/two-shot kernel of
   ``comm/xgmi.py`` on a side stream instead of an RCCL ring (latency-bound sizes).
+* ``force_collectives`` (or env ``DTD_FORCE_COLLECTIVES=1``) issues the bucket all-reduces even
+  on a one-rank process group, so the N > 1 data path -- RCCL kernels on RCCL's stream, launched
+  from the autograd thread while backward runs, waited for by the compute stream, and captured
+  in a hipGraph with the rest of the step -- runs and is measured on a single GPU.
 * The constructor broadcasts parameters from rank 0 (C3).  Per-step buffer broadcast (C4) is
   elided: the only module buffers of the reference models are constant index tensors.
 """
@@ -70,11 +74,19 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, bucket_cap_mb: float = 25.0,
                  grad_dtype: torch.dtype | None = None, process_group=None, broadcast_parameters: bool = True,
                  overlap: bool = True, flatten_params: bool = True, small_bucket_allreduce: str = "rccl",
-                 xgmi_max_mb: float = 4.0, async_wgrad: bool = False, xgmi_check_every: int = 100):
+                 xgmi_max_mb: float = 4.0, async_wgrad: bool = False, xgmi_check_every: int = 100,
+                 force_collectives: bool | None = None):
         super().__init__()
         self.module = module
         self.process_group = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        if force_collectives is None:
+            force_collectives = os.environ.get("DTD_FORCE_COLLECTIVES", "0") == "1"
+        if force_collectives and not dist.is_initialized():
+            raise RuntimeError("force_collectives needs an initialised process group (comm.init())")
+        # collectives run whenever there is a peer -- or always, when forced (one-GPU rehearsal of
+        # the multi-GPU data path)
+        self.collectives = self.world > 1 or bool(force_collectives)
         self.overlap = overlap
         params = [p for p in module.parameters() if p.requires_grad]
         # reverse registration order ~ gradient-ready order in backward (torch DDP does the same)
@@ -186,7 +198,7 @@ class DistributedDataParallel(nn.Module):
             self._launch(self.buckets[k])
 
     def _launch(self, b: _Bucket) -> None:
-        if self.world == 1:
+        if not self.collectives:
             return
         view = self.grads.buf[b.start:b.end]
         if self._xgmi is not None and self._xgmi.supports(view):

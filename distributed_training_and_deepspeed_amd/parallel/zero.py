@@ -59,7 +59,8 @@ DEFAULTS = {
     "comms_logger": {"enabled": False},
     "zero_optimization": {"stage": 0, "reduce_bucket_size": 5e8, "allgather_bucket_size": 5e8,
                           "overlap_comm": None, "stage3_prefetch_bucket_size": 5e7,
-                          "overlap_param_refresh": True, "world1_replicated": True},
+                          "overlap_param_refresh": True, "world1_replicated": True,
+                          "force_collectives": False, "stage3_gather_communicator": False},
 }
 
 
@@ -86,6 +87,14 @@ class ZeroConfig:
         self.prefetch_bucket = max(0, int(float(z.get("stage3_prefetch_bucket_size", 5e7))))
         self.overlap_refresh = bool(z.get("overlap_param_refresh", True))
         self.world1_replicated = bool(z.get("world1_replicated", True))
+        # issue every collective even on a one-rank group (one-GPU rehearsal of the N > 1 path)
+        self.force_collectives = (bool(z.get("force_collectives", False))
+                                  or os.environ.get("DTD_FORCE_COLLECTIVES", "0") == "1")
+        # stage 3 gathers on a second communicator beside the reduce-scatters: off by default --
+        # RCCL documents that concurrent communicators on one device can deadlock when their
+        # kernels cannot all be resident; the gathers then share the main group and its stream
+        # order (they still run on their own HIP stream, fenced by events)
+        self.gather_communicator = bool(z.get("stage3_gather_communicator", False))
         oc = z.get("overlap_comm")
         self.overlap = (self.stage >= 2) if oc is None else bool(oc)
         bf = cfg.get("bf16", {})
@@ -244,7 +253,7 @@ class ZeroEngine(nn.Module):
         # process group), so a prefetch gather does not queue behind a reduce-scatter
         self.gather_stream = torch.cuda.Stream(self.device) if (self.cuda and self.stage == 3) else None
         self.gather_group = process_group
-        if self.stage == 3 and self.world > 1:
+        if self.stage == 3 and self.world > 1 and self.config.gather_communicator:
             ranks = dist.get_process_group_ranks(process_group) if process_group is not None \
                 else list(range(self.world))
             self.gather_group = dist.new_group(ranks=ranks)
@@ -261,6 +270,13 @@ class ZeroEngine(nn.Module):
         # views of its (whole) shard, so nothing is copied per use (one micro-batch per step)
         self.alias_units = (self.stage == 3 and self.world == 1 and self.config.world1_replicated
                             and self.config.gas == 1)
+        # collectives run with a peer, or always when forced (world-1 rehearsal of the RCCL path)
+        self.collect = self.world > 1 or self.config.force_collectives
+        if self.collect and self.world == 1:
+            # the partitioned data flow (stage 0 keeps its all-reduce), so the reduce-scatters and
+            # all-gathers of stages 1-3 actually run
+            self.replicated = self.stage == 0
+            self.alias_units = False
         self.micro_step = 0
         self.global_steps = 0
         self._callback_queued = False
@@ -438,12 +454,16 @@ class ZeroEngine(nn.Module):
                     p.main_grad = s.view(s.gbuf, i)
                 off += s.numel
         # ring arenas: gradient landing regions (stages 2/3) and gathered units (stage 3)
-        reg = [s.numel for s in self.segments if (self.stage >= 2 and not self.replicated) or s.unit]
-        big_unit = max([s.numel for s in self.units], default=0)
-        self.landing = _Arena(max(4 * max(self.config.reduce_bucket, ALIGN), 3 * big_unit) if reg else 0,
-                              self.grad_dtype, dev)
-        self.gather_arena = _Arena(max(self.config.prefetch_bucket + 2 * big_unit, 4 * big_unit) if self.units else 0,
-                                   dt, dev)
+        # (aliased stage-3 units land in their own shard and gather nothing: no arena for them).
+        # The landing arena never exceeds the regions it can hold at once -- the whole gradient
+        # -- so a large reduce_bucket_size on a small model does not pin more than that.
+        reg = [s.numel for s in self.segments
+               if (s.unit and not self.alias_units) or (not s.unit and self.stage >= 2 and not self.replicated)]
+        big_unit = 0 if self.alias_units else max([s.numel for s in self.units], default=0)
+        want = max(4 * max(self.config.reduce_bucket, ALIGN), 3 * big_unit)
+        self.landing = _Arena(min(want, sum(reg)) if reg else 0, self.grad_dtype, dev)
+        self.gather_arena = _Arena(max(self.config.prefetch_bucket + 2 * big_unit, 4 * big_unit)
+                                   if self.units and not self.alias_units else 0, dt, dev)
         # master shard: chunk `shard_rank` of every segment
         for s in self.buckets:
             lo = self.shard_rank * s.chunk
@@ -536,11 +556,29 @@ class ZeroEngine(nn.Module):
             return
         cur = torch.cuda.current_stream(self.device) if self.cuda else None
         s.gbuf = self.landing.acquire(s.numel, s.index, waiter=cur.wait_event if cur is not None else None)
-        # padding (alignment gaps, segment tail) must reduce as zeros: the region is recycled
-        s.gbuf.zero_()
+        # padding (alignment gaps, segment tail) must reduce as zeros: the region is recycled.  Only
+        # the padding is cleared (one index_fill_ launch): every parameter's own range is written
+        # in full by its first contribution (grad_dst: accumulate=False) or zeroed in
+        # _reduce_segment when the parameter got no gradient
+        pad = self._pad_index(s)
+        if pad is not None:
+            s.gbuf.index_fill_(0, pad, 0)
         for i, p in enumerate(s.params):
             p.main_grad = s.view(s.gbuf, i)
             p._dtd_touched = False
+
+    def _pad_index(self, s: _Segment):
+        """Positions of segment ``s`` outside every parameter (alignment gaps and the tail),
+        cached on the device; None when there are none."""
+        cache = self.__dict__.setdefault("_pads", {})
+        if s.index not in cache:
+            idx, off = [], 0
+            for i, shape in enumerate(s.shapes):
+                n = math.prod(shape)
+                end = s.offsets[i + 1] if i + 1 < len(s.shapes) else s.numel
+                idx.extend(range(s.offsets[i] + n, end))
+            cache[s.index] = torch.tensor(idx, dtype=torch.long, device=self.device) if idx else None
+        return cache[s.index]
 
     def _expect(self, p) -> None:
         self.tracker.expect(self._pindex[id(p)])
@@ -582,7 +620,7 @@ class ZeroEngine(nn.Module):
         out = self.gshard[s.shard_off:s.shard_off + s.chunk]
         with self._comm_ctx():
             if self.replicated:  # buf aliases the gradient "shard" (the full buffer)
-                if self.world > 1:
+                if self.collect:
                     op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
                     w = clog.all_reduce(buf, op=op, group=self.group, async_op=True)
                     w.wait()
@@ -590,7 +628,7 @@ class ZeroEngine(nn.Module):
                         buf.div_(self.world)
             else:
                 dst = out if first else self._tmp()[s.shard_off:s.shard_off + s.chunk]
-                if self.world > 1:
+                if self.collect:
                     op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
                     w = clog.reduce_scatter_tensor(dst, buf, op=op, group=self.group, async_op=True)
                     w.wait()
@@ -648,7 +686,7 @@ class ZeroEngine(nn.Module):
         full = self.gather_arena.acquire(s.numel, s.index)
         src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
         with self._comm_ctx(self.gather_stream):   # the stream wait orders it behind earlier reads
-            if self.world > 1:
+            if self.collect:
                 w = clog.all_gather_into_tensor(full, src, group=self.gather_group, async_op=True)
                 w.wait()
             else:
@@ -806,7 +844,7 @@ class ZeroEngine(nn.Module):
             with self._comm_ctx():
                 outs = [s.full for s in grp]
                 ins = [self.lowp_view[s.shard_off:s.shard_off + s.chunk] for s in grp]
-                if self.world > 1:
+                if self.collect:
                     w = clog.all_gather_coalesced(outs, ins, group=self.group, async_op=True)
                     w.wait()
                 else:

@@ -1,0 +1,8 @@
+#!/usr/bin/env bash
+cd "${GRAFT_REPO_ROOT}"
+source scripts/gpu_step.sh
+export TMPDIR=/tmp
+step bench_default 300 python bench.py
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step prof_default 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_default -o run --output-format csv -- python bench.py --steps 5 --warmup 2
+echo done

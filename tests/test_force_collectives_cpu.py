@@ -1,0 +1,65 @@
+"""One-rank rehearsal of the N > 1 data path (``force_collectives``), CPU / gloo.
+
+At world 1 DDP and ZeRO normally skip their collectives (an all-reduce over one rank is an
+identity).  With ``force_collectives`` they issue them anyway -- the path the GPU bench
+(``bench.py --force-collectives``) uses to put real RCCL kernels inside a measured 1-GPU step.
+Checked here: the collectives are issued (comms logger), the results equal the unforced run,
+and the ZeRO-2 landing arena (a) is capped at the gradient size and (b) only needs its padding
+cleared (the arena is filled with NaN before training; a leaked NaN would poison the shards).
+"""
+import math
+
+import torch
+import torch.multiprocessing as mp
+
+from . import dist_workers as W
+from .conftest import pick_free_port
+
+
+def _spawn(fn, world, *args):
+    mp.spawn(fn, args=(world,) + args, nprocs=world, join=True)
+
+
+def test_ddp_force_collectives_world1(tmp_path):
+    _spawn(W.ddp_worker, 1, pick_free_port(), str(tmp_path), "tiny", "fused", 2, 0.05, False, "_plain")
+    _spawn(W.ddp_worker, 1, pick_free_port(), str(tmp_path), "tiny", "fused", 2, 0.05, True, "_forced")
+    plain = torch.load(tmp_path / "ddp_plain.pt", weights_only=True)
+    forced = torch.load(tmp_path / "ddp_forced.pt", weights_only=True)
+    assert "all_reduce" not in plain["comms"]
+    n_buckets = len(forced["buckets"])
+    assert n_buckets > 1 and sum(forced["comms"]["all_reduce"].values()) == 2 * n_buckets
+    for n, g in plain["grads0"].items():
+        assert torch.equal(g, forced["grads0"][n]), n
+    for n, p in plain["params"].items():
+        assert torch.equal(p, forced["params"][n]), n
+
+
+def test_zero_force_collectives_world1(tmp_path):
+    for stage in (1, 2, 3):
+        _spawn(W.zero_worker, 1, pick_free_port(), str(tmp_path), "causal-tiny", stage, 2, 2, 0.0, "_plain")
+        _spawn(W.zero_worker, 1, pick_free_port(), str(tmp_path), "causal-tiny", stage, 2, 2, 0.0, "_forced",
+               True, True)
+        plain = torch.load(tmp_path / f"zero{stage}_plain.pt", weights_only=True)
+        forced = torch.load(tmp_path / f"zero{stage}_forced.pt", weights_only=True)
+        assert "reduce_scatter_tensor" in forced["comms"], (stage, forced["comms"])
+        assert "all_gather_into_tensor" in forced["comms"], (stage, forced["comms"])
+        assert "reduce_scatter_tensor" not in plain["comms"]
+        # the same parameters, whatever the layout: compare the multiset of parameter tensors
+        def params(res):
+            out = []
+            for unit, numel, chunk, off, shapes in res["layout"]:
+                full = res["shards"][0][off:off + chunk]
+                o = 0
+                for shp in shapes:
+                    n = math.prod(shp)
+                    out.append((tuple(shp), full[o:o + n].clone()))
+                    o += -(-n // 64) * 64
+            out.sort(key=lambda t: (t[0], t[1].sum().item()))
+            return out
+        a, b = params(plain), params(forced)
+        assert len(a) == len(b)
+        for (s1, x), (s2, y) in zip(a, b):
+            assert s1 == s2 and torch.isfinite(y).all()
+            assert torch.allclose(x, y, atol=3e-5, rtol=1e-4), (stage, s1, (x - y).abs().max().item())
+        if stage >= 2:
+            assert 0 < forced["landing_numel"] <= forced["grad_numel"]
