@@ -185,16 +185,31 @@ def broadcast(tensor, src=0, group=None, async_op=False):
                             tensor, _nbytes(tensor), group, async_op)
 
 
+def _gloo_cuda(t: torch.Tensor, group) -> bool:
+    """gloo on GPU tensors (several ranks sharing one GPU in tests): gloo implements all_reduce /
+    all_gather for device tensors but not the fused-buffer reduce-scatter / all-gather forms."""
+    return t.is_cuda and dist.is_initialized() and dist.get_backend(group) == "gloo"
+
+
 def reduce_scatter_tensor(output, input, op=dist.ReduceOp.SUM, group=None, async_op=False):
-    return comms_logger.run("reduce_scatter_tensor",
-                            lambda a: dist.reduce_scatter_tensor(output, input, op=op, group=group, async_op=a),
-                            input, _nbytes(input), group, async_op)
+    def fn(a):
+        if _gloo_cuda(input, group):   # all-reduce a copy, keep this rank's chunk
+            tmp = input.clone()
+            dist.all_reduce(tmp, op=op, group=group)
+            output.copy_(tmp.view(dist.get_world_size(group), -1)[dist.get_rank(group)].view_as(output))
+            return _DoneWork() if a else None
+        return dist.reduce_scatter_tensor(output, input, op=op, group=group, async_op=a)
+    return comms_logger.run("reduce_scatter_tensor", fn, input, _nbytes(input), group, async_op)
 
 
 def all_gather_into_tensor(output, input, group=None, async_op=False):
-    return comms_logger.run("all_gather_into_tensor",
-                            lambda a: dist.all_gather_into_tensor(output, input, group=group, async_op=a),
-                            output, _nbytes(output), group, async_op)
+    def fn(a):
+        if _gloo_cuda(output, group):   # list form into row views of the output
+            dist.all_gather(list(output.view(dist.get_world_size(group), -1).unbind(0)), input.reshape(-1),
+                            group=group)
+            return _DoneWork() if a else None
+        return dist.all_gather_into_tensor(output, input, group=group, async_op=a)
+    return comms_logger.run("all_gather_into_tensor", fn, output, _nbytes(output), group, async_op)
 
 
 class _MultiWork:
@@ -228,6 +243,10 @@ def all_gather_coalesced(outputs, inputs, group=None, async_op=False):
                 return cm
             cm.wait()
             return None
+        if outputs and _gloo_cuda(outputs[0], group):
+            for o, i in zip(outputs, inputs):
+                all_gather_into_tensor(o, i, group=group)
+            return _DoneWork() if a else None
         works = [dist.all_gather_into_tensor(o, i, group=group, async_op=a) for o, i in zip(outputs, inputs)]
         return _MultiWork(works) if a else None
 

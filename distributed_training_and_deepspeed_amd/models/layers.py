@@ -71,7 +71,8 @@ class LayerNorm(nn.Module):
         self.eps, self.rt = eps, rt
 
     def forward(self, x):
-        if self.rt.use_fused(x):
+        self._dtd_weightless_bwd = self.rt.use_fused(x)   # see TransformerLayer.forward
+        if self._dtd_weightless_bwd:
             note_use((self.weight, self.bias))
             return _LNFn.apply(x, self.weight, self.bias, self.eps)
         return F.layer_norm(x, (x.shape[-1],), self.weight, self.bias, self.eps)
@@ -143,6 +144,8 @@ class _EmbedFn(torch.autograd.Function):
 
 
 class Embeddings(nn.Module):
+    token_input = True   # takes integer token ids (no input gradient): parallel/pipeline.py idle hooks
+
     def __init__(self, cfg: TransformerConfig, rt: Runtime):
         super().__init__()
         self.cfg, self.rt = cfg, rt
@@ -168,7 +171,8 @@ class Embeddings(nn.Module):
         return tuple(p for p in (self.word, self.pos, self.tok_type, self.ln_g, self.ln_b) if p is not None)
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
-        if self.rt.use_fused(self.word):
+        self._dtd_weightless_bwd = self.rt.use_fused(self.word)   # see TransformerLayer.forward
+        if self._dtd_weightless_bwd:
             note_use(self.params())
             return _EmbedFn.apply(ids, self, *self.params())
         c = self.cfg
@@ -275,6 +279,8 @@ class MLMHead(nn.Module):
 
     def forward(self, x: torch.Tensor, labels: torch.Tensor | None = None) -> torch.Tensor:
         """Loss when labels are given, else logits (module call so ZeRO-3 unit hooks fire)."""
+        # only the fused loss path keeps no weight views for the backward (TransformerLayer.forward)
+        self._dtd_weightless_bwd = labels is not None and self.rt.use_fused(x)
         return self.loss(x, labels) if labels is not None else self.logits(x)
 
     def logits(self, x: torch.Tensor) -> torch.Tensor:
@@ -376,6 +382,7 @@ class LMHead(nn.Module):
         return self._tied[0]
 
     def forward(self, x: torch.Tensor, labels: torch.Tensor | None = None) -> torch.Tensor:
+        self._dtd_weightless_bwd = labels is not None and self.rt.use_fused(x)   # TransformerLayer.forward
         return self.loss(x, labels) if labels is not None else self.logits(x)
 
     def logits(self, x):

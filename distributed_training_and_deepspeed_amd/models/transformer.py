@@ -172,7 +172,10 @@ class TransformerLayer(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x: [B, S, h] -> [B, S, h]"""
-        if self.rt.use_fused(x):
+        # the fused backward reads the parameters at backward time (no saved weight views): ZeRO-3
+        # may release and later re-gather them in between (parallel/zero.py)
+        self._dtd_weightless_bwd = self.rt.use_fused(x)
+        if self._dtd_weightless_bwd:
             note_use(self.params())
             return _FusedLayerFn.apply(x, self, *self.params())
         return self._reference(x)

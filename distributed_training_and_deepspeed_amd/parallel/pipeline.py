@@ -132,8 +132,30 @@ def attach_idle_hooks(groups: list[list[nn.Module]], tracker: IdleTimeTracker) -
         first, last = g[0], g[-1]
         first.register_forward_pre_hook(lambda m, a, i=idx: tracker.mark(i, True, True))
         last.register_forward_hook(lambda m, a, o, i=idx: tracker.mark(i, True, False))
-        last.register_full_backward_pre_hook(lambda m, go, i=idx: tracker.mark(i, False, True))
-        first.register_full_backward_hook(lambda m, gi, go, i=idx: tracker.mark(i, False, False))
+        if getattr(last, "token_input", False):   # a group of the embeddings alone
+            def _bwd_start(m, a, o, i=idx):
+                if torch.is_tensor(o) and o.requires_grad:
+                    o.register_hook(lambda g: tracker.mark(i, False, True))
+            last.register_forward_hook(_bwd_start)
+        else:
+            last.register_full_backward_pre_hook(lambda m, go, i=idx: tracker.mark(i, False, True))
+        if getattr(first, "token_input", False):
+            # the group starts at the embeddings, whose inputs (token ids) take no gradient: a full
+            # backward hook there would fire when the gradient of its OUTPUT arrives -- the START
+            # of its backward.  The embeddings' backward is the last work of the whole backward
+            # pass, so the group's backward ends when the autograd engine finishes: mark it from
+            # an engine callback queued when that backward starts.
+            # (A tensor hook on the embeddings' output, not a module backward hook: torch warns
+            # and misfires module backward hooks on a module whose inputs take no gradient.)
+            def _queue_end(g, i=idx):
+                torch.autograd.Variable._execution_engine.queue_callback(lambda: tracker.mark(i, False, False))
+
+            def _watch_output(m, a, o, cb=_queue_end):
+                if torch.is_tensor(o) and o.requires_grad:
+                    o.register_hook(cb)
+            first.register_forward_hook(_watch_output)
+        else:
+            first.register_full_backward_hook(lambda m, gi, go, i=idx: tracker.mark(i, False, False))
 
 
 class GPipe(nn.Module):

@@ -95,6 +95,10 @@ class ZeroConfig:
         # kernels cannot all be resident; the gathers then share the main group and its stream
         # order (they still run on their own HIP stream, fenced by events)
         self.gather_communicator = bool(z.get("stage3_gather_communicator", False))
+        # race / stale-reference detector: fill every released stage-3 gather region
+        # with NaN, so a read through a stale view of released weights poisons the result
+        self.poison_released = (bool(z.get("debug_poison_released", False))
+                                or os.environ.get("DTD_ZERO_POISON", "0") == "1")
         oc = z.get("overlap_comm")
         self.overlap = (self.stage >= 2) if oc is None else bool(oc)
         bf = cfg.get("bf16", {})
@@ -103,7 +107,7 @@ class ZeroConfig:
 
 class _Segment:
     __slots__ = ("index", "params", "shapes", "offsets", "numel", "chunk", "shard_off", "full", "gbuf", "ready",
-                 "launched", "unit", "gather_event", "module", "pending_release", "first_use")
+                 "launched", "unit", "gather_event", "module", "pending_release", "first_use", "hold")
 
     def __init__(self, index, params, world):
         self.index = index
@@ -125,6 +129,7 @@ class _Segment:
         self.gather_event = None
         self.module = None
         self.pending_release = False
+        self.hold = False     # stage 3: kept gathered from its forward until its own backward reduced
         self.first_use = 0    # forward position of the first unit that reads this segment
 
     def view(self, flat: torch.Tensor, i: int) -> torch.Tensor:
@@ -712,6 +717,8 @@ class ZeroEngine(nn.Module):
             torch.cuda.current_stream(self.device).wait_event(s.gather_event)
             s.gather_event = None
         if not self.alias_units:
+            if self.config.poison_released and s.full.is_floating_point():
+                s.full.fill_(float("nan"))
             self.gather_arena.release(s.full, None,
                                       torch.cuda.current_stream(self.device) if self.cuda else None)
         self._set_released(s)
@@ -742,6 +749,14 @@ class ZeroEngine(nn.Module):
                 t = out if torch.is_tensor(out) else None
                 if t is not None and t.requires_grad:
                     t.register_hook(self._make_bwd_start(k))
+                if not getattr(mod, "_dtd_weightless_bwd", False):
+                    # plain autograd ops saved VIEWS of the gathered weights for the backward
+                    # (F.linear keeps weight.t()); those views do not follow a re-gather, and the
+                    # arena would hand their bytes to the next unit.  Keep the unit gathered until
+                    # its own backward has reduced (pending release).  The fused modules' backward
+                    # re-reads the parameters themselves and declares _dtd_weightless_bwd.
+                    s.hold = True
+                    return
             self._release(s)
         return hook
 
@@ -764,10 +779,11 @@ class ZeroEngine(nn.Module):
             return
         self._reduce_segment(s)
         s.pending_release = True
+        s.hold = False
 
     def _release_pending(self, keep=()) -> None:
         for u in self.units:
-            if u.pending_release and u not in keep:
+            if u.pending_release and not u.hold and u not in keep:
                 u.pending_release = False
                 self._release(u)
 

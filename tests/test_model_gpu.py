@@ -46,6 +46,38 @@ def test_fused_gpu_matches_reference(name, extra, dtype):
         assert err < gtol, f"{n}: rel err {err}"
 
 
+@pytest.mark.parametrize("name,extra", CASES)
+def test_fused_bf16_gradients_track_fused_fp32(name, extra):
+    """Per-tensor bound on the bf16 fused path: its gradients against an fp32 run of the SAME
+    fused graph on the SAME (bf16-representable) weights and dropout masks, so the only difference
+    is compute precision.  Every parameter's gradient must be within 3 % (relative L2) -- a real
+    backward bug in any single small tensor (a bias, an LN gamma) shows up here, where the loose
+    bf16-vs-CPU-reference bound above would hide it."""
+    cfg = C.get_config(name).with_(**extra, hidden_dropout=0.1, attn_dropout=0.1)
+    C.PRESETS["_t"] = cfg
+    f32 = build_model("_t", impl="fused", seed=3, device="cuda")
+    with torch.no_grad():
+        for p in f32.parameters():
+            p.copy_(p.to(torch.bfloat16).float())   # weights both runs represent exactly
+    b16 = build_model("_t", impl="fused", seed=3, device="cuda")
+    b16.load_state_dict(f32.state_dict())
+    b16.to(torch.bfloat16)
+    ds = SyntheticLMDataset(cfg, 4, seq_len=128, seed=5)
+    ids, lab = ds.input_ids.cuda(), ds.labels.cuda()
+    l32 = f32(ids, labels=lab).loss
+    l32.backward()
+    l16 = b16(ids, labels=lab).loss
+    l16.backward()
+    assert abs(l32.item() - l16.item()) <= 1e-2 * abs(l32.item())
+    worst = []
+    for (n, p1), (_, p2) in zip(f32.named_parameters(), b16.named_parameters()):
+        g1, g2 = p1.grad.float(), p2.grad.float()
+        err = (g1 - g2).norm().item() / (g1.norm().item() + 1e-12)
+        worst.append((err, n))
+    worst.sort(reverse=True)
+    assert worst[0][0] <= 0.03, f"largest per-tensor gradient errors: {worst[:5]}"
+
+
 def test_bert_base_training_loss_decreases():
     from distributed_training_and_deepspeed_amd.optim import hf_adamw
     from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
