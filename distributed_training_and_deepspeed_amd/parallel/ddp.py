@@ -135,10 +135,52 @@ class DistributedDataParallel(nn.Module):
             self._broadcast_params()
 
     # ------------------------------------------------------------------ setup
+    def _trailing_start(self) -> int:
+        """Layout index from which every parameter belongs to the model's first unit (the
+        embeddings, incl. a tied decoder weight): their gradients are complete only when the whole
+        backward is, so they form the trailing bucket(s) of the step.  len(params) if none."""
+        units = self.module.zero3_units() if hasattr(self.module, "zero3_units") else []
+        if not units:
+            return len(self.layout.params)
+        first = {id(p) for p in units[0].parameters()}
+        i = len(self.layout.params)
+        while i > 0 and id(self.layout.params[i - 1]) in first:
+            i -= 1
+        return i
+
     def _build_buckets(self, cap_mb: float) -> None:
-        cap = int(cap_mb * 1024 * 1024 / self.grads.buf.element_size())
+        """Consecutive buckets of <= cap over the layout (reverse registration ~ backward order),
+        with a shaped tail for the multi-GPU critical path: the trailing group (embeddings: ready
+        only when backward ends) gets bucket(s) of its own, and the parameters just before it (the
+        first layer) a small bucket of <= tail_bucket_mb, launched as soon as that layer's
+        backward ends so its all-reduce finishes under the embedding backward.  What is exposed
+        after backward is then the embedding all-reduce alone, not a full bucket of layer
+        gradients queued in front of it.  DTD_DDP_TAIL_BUCKET_MB=0 disables the shaping."""
+        es = self.grads.buf.element_size()
+        cap = int(cap_mb * 1024 * 1024 / es)
+        tail_cap = int(float(os.environ.get("DTD_DDP_TAIL_BUCKET_MB", "16")) * 1024 * 1024 / es)
         L = self.layout
-        bucket_of, ranges = assign_buckets(L.offsets, [p.numel() for p in L.params], L.numel, cap)
+        n = len(L.params)
+        numels = [p.numel() for p in L.params]
+        cuts = [0, n]
+        t = self._trailing_start() if tail_cap > 0 else n
+        if 0 < t < n:
+            cuts = [0, t, n]
+            # the small pre-trailing bucket: the parameters before t that fit in tail_cap
+            j, size = t, 0
+            while j > 0 and size + numels[j - 1] <= tail_cap:
+                size += numels[j - 1]
+                j -= 1
+            if 0 < j < t:
+                cuts = [0, j, t, n]
+        bucket_of, ranges = [], []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            lo = L.offsets[a]
+            hi = L.offsets[b] if b < n else L.numel
+            bo, rg = assign_buckets([o - lo for o in L.offsets[a:b]], numels[a:b], hi - lo, cap)
+            base = len(ranges)
+            bucket_of += [base + k for k in bo]
+            ranges += [(lo + s0, lo + e0) for s0, e0 in rg]
         members = [[] for _ in ranges]
         for i, b in enumerate(bucket_of):
             members[b].append(L.params[i])

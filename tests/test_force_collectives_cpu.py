@@ -63,3 +63,25 @@ def test_zero_force_collectives_world1(tmp_path):
             assert torch.allclose(x, y, atol=3e-5, rtol=1e-4), (stage, s1, (x - y).abs().max().item())
         if stage >= 2:
             assert 0 < forced["landing_numel"] <= forced["grad_numel"]
+
+
+def test_ddp_tail_buckets_shape_bert_base():
+    """Multi-GPU critical path: the embeddings (ready only when backward ends) get their own final
+    bucket, and the first layer's gradients a small bucket just before it, so the all-reduce
+    exposed after backward is the embedding one alone."""
+    import os
+    from distributed_training_and_deepspeed_amd.models import build_model
+    from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
+    m = build_model("base", dtype=torch.bfloat16, seed=0)
+    d = DistributedDataParallel(m, bucket_cap_mb=64)
+    emb = {id(p) for p in m.embeddings.parameters()}
+    last, prev = d.buckets[-1], d.buckets[-2]
+    assert {id(p) for p in last.params} == emb
+    assert (prev.end - prev.start) * 2 <= 16 * 2 ** 20 and not any(id(p) in emb for p in prev.params)
+    assert all((b.end - b.start) * 2 <= 64 * 2 ** 20 for b in d.buckets)
+    os.environ["DTD_DDP_TAIL_BUCKET_MB"] = "0"
+    try:
+        d0 = DistributedDataParallel(build_model("base", dtype=torch.bfloat16, seed=0), bucket_cap_mb=64)
+        assert len(d0.buckets) < len(d.buckets)
+    finally:
+        del os.environ["DTD_DDP_TAIL_BUCKET_MB"]
