@@ -92,7 +92,7 @@ def prefetch_masks(layers, input_ids: torch.Tensor) -> None:
     """Issue every layer's attention-dropout mask generation (fused bf16 path only)."""
     B, S = input_ids.shape[0], input_ids.shape[1]
     for layer in layers:
-        if layer.rt.use_fused(input_ids) and layer.qkv_w.dtype == torch.bfloat16:
+        if layer.rt.use_fused(input_ids) and layer.qkv_w.dtype in (torch.bfloat16, torch.float32):
             layer.prefetch_attention_masks(B, S, input_ids.device)
 
 
@@ -262,7 +262,7 @@ class _FusedLayerFn(torch.autograd.Function):
             pend = pre[3]
         else:
             pend = A.attn_masks_async(B, S, H, D, p_a, rng, sa, x.device) \
-                if x.is_cuda and x.dtype == torch.bfloat16 else None
+                if x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) else None
         if c.pre_ln:
             _, a_in, m1, r1 = Fx.ln_fwd(None, x2d, g1, b1, eps, 0.0, rng, 0)
         else:

@@ -65,6 +65,9 @@ _SIGS = {
     "dtd_attn_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, U32, P]),
     "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, P]),
     "dtd_attn_masks": (I, [P, I, I, I, F, P, U32, P]),
+    # attention_f32.hip
+    "dtd_attn_fwd_f32": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
+    "dtd_attn_bwd_f32": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
     # softmax.hip
     "dtd_softmax_fwd": (I, [I, P, P, I, I, P]),
     "dtd_softmax_bwd": (I, [I, P, P, P, I, I, P]),

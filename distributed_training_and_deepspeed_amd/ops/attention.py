@@ -41,8 +41,14 @@ def _split(qkv, B, S, H, D):
     return x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
 
 
+def _cdt(t: torch.Tensor) -> torch.dtype:
+    """Compute dtype of the math reference: fp64 for fp64 inputs (kernel tests), else fp32."""
+    return torch.float64 if t.dtype == torch.float64 else torch.float32
+
+
 def _scores(q, k, scale, causal, slopes):
-    s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
+    c = _cdt(q)
+    s = torch.matmul(q.to(c), k.to(c).transpose(-1, -2)) * scale
     S = q.shape[2]
     if slopes is not None:
         s = s + slopes.to(s.device).view(1, -1, 1, 1) * torch.arange(S, device=s.device, dtype=s.dtype).view(1, 1, 1, S)
@@ -66,7 +72,7 @@ def attn_fwd_ref(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngStat
     prob = torch.exp(s - lse[..., None])
     if p > 0:
         prob = prob * _drop_mask(B, H, S, p, rng, sid, qkv.device) / (1.0 - p)
-    ctx = torch.matmul(prob, v.float())  # [B,H,S,D]
+    ctx = torch.matmul(prob, v.to(prob.dtype))  # [B,H,S,D]
     return ctx.transpose(1, 2).reshape(B * S, H * D).to(qkv.dtype), lse
 
 
@@ -74,21 +80,22 @@ def attn_bwd_ref(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     q, k, v = _split(qkv, B, S, H, D)
     s = _scores(q, k, scale, causal, slopes)
-    prob = torch.exp(s - lse[..., None])
-    do = dctx.view(B, S, H, D).transpose(1, 2).float()
-    o = ctx.view(B, S, H, D).transpose(1, 2).float()
+    prob = torch.exp(s - lse[..., None].to(s.dtype))
+    c = s.dtype
+    do = dctx.view(B, S, H, D).transpose(1, 2).to(c)
+    o = ctx.view(B, S, H, D).transpose(1, 2).to(c)
     if p > 0:
-        keep = _drop_mask(B, H, S, p, rng, sid, qkv.device).float() / (1.0 - p)
+        keep = _drop_mask(B, H, S, p, rng, sid, qkv.device).to(c) / (1.0 - p)
         pd = prob * keep
     else:
         keep, pd = None, prob
     dv = torch.matmul(pd.transpose(-1, -2), do)
-    dpd = torch.matmul(do, v.float().transpose(-1, -2))
+    dpd = torch.matmul(do, v.to(c).transpose(-1, -2))
     dp = dpd * keep if keep is not None else dpd
     delta = (do * o).sum(-1, keepdim=True)
     ds = prob * (dp - delta)
-    dq = torch.matmul(ds, k.float()) * scale
-    dk = torch.matmul(ds.transpose(-1, -2), q.float()) * scale
+    dq = torch.matmul(ds, k.to(c)) * scale
+    dk = torch.matmul(ds.transpose(-1, -2), q.to(c)) * scale
     dqkv = torch.stack([dq, dk, dv], dim=2)  # [B,H,3,S,D]
     return dqkv.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * H * D).to(qkv.dtype)
 
@@ -105,6 +112,19 @@ def _warn_once():
 
 def kernel_supported(qkv: torch.Tensor, D: int) -> bool:
     return qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128) and _lib.has("dtd_attn_fwd")
+
+
+def f32_kernel_supported(qkv: torch.Tensor, D: int) -> bool:
+    """The reference-precision kernels (ops/csrc/attention_f32.hip: exact f32 MFMA products)."""
+    return (qkv.is_cuda and qkv.dtype == torch.float32 and D in (64, 128) and _lib.has("dtd_attn_fwd_f32")
+            and _lib.has("dtd_attn_masks"))
+
+
+def _masks_now(B, S, H, p, rng, sid, device) -> torch.Tensor:
+    """Dropout keep bits generated on the current stream (the fp32 path)."""
+    masks = torch.empty((2, mask_words(B, H, S)), dtype=torch.int32, device=device)
+    _lib.call("dtd_attn_masks", masks.data_ptr(), B, S, H, float(p), rng.state.data_ptr(), sid, _lib.stream())
+    return masks
 
 
 _SIDE = {}
@@ -178,6 +198,8 @@ def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | 
     """Returns (ctx [B*S, H*D], lse [B, H, S] fp32, masks).  ``masks`` holds the dropout keep
     bits for the backward ([2, B*H*S*ceil(S/32)] int32 on the kernel path, None otherwise);
     pass the ``attn_masks_async`` result to reuse masks generated ahead on a side stream."""
+    if f32_kernel_supported(qkv, D):
+        return _attn_fwd_f32(qkv, B, S, H, D, causal, slopes, p, rng, sid, masks)
     if not kernel_supported(qkv, D):
         if qkv.is_cuda and qkv.dtype == torch.bfloat16 and _lib.has("dtd_attn_fwd") is False:
             _warn_once()
@@ -211,6 +233,11 @@ def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, 
     column sums of dqkv (the qkv projection's bias gradient) -- on the kernel path as per-wave
     partials from the dQ / dK,dV epilogues (no extra pass over dqkv)."""
     from . import functional as Fx
+    if f32_kernel_supported(qkv, D) and (p <= 0 or masks is not None):
+        dqkv = _attn_bwd_f32(dctx, qkv, ctx, lse, B, S, H, D, causal, slopes, p, masks)
+        if dbias is not None:
+            Fx.bias_grad(dqkv, *dbias)
+        return dqkv
     if not kernel_supported(qkv, D):
         dqkv = attn_bwd_ref(dctx, qkv, ctx, lse, B, S, H, D, causal, slopes, p, rng, sid)
         if dbias is not None:
@@ -237,4 +264,38 @@ def attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal=False, slopes=None, p=0.0, 
             Fx._finalize(part, part.shape[0], ld, (dst, acc), acc)
         else:
             Fx.bias_grad(dqkv, *dbias)
+    return dqkv
+
+
+def _attn_fwd_f32(qkv, B, S, H, D, causal, slopes, p, rng, sid, masks):
+    qkv = qkv.contiguous()
+    ctx = torch.empty((B * S, H * D), dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+    if p > 0:
+        if masks is not None:
+            torch.cuda.current_stream(qkv.device).wait_event(masks.event)
+            masks = masks.masks
+        else:
+            masks = _masks_now(B, S, H, p, rng, sid, qkv.device)
+    else:
+        masks = None
+    sl = slopes.to(device=qkv.device, dtype=torch.float32).contiguous() if slopes is not None else None
+    ld, es, base = 3 * H * D, qkv.element_size(), qkv.data_ptr()
+    _lib.call("dtd_attn_fwd_f32", base, base + H * D * es, base + 2 * H * D * es, ctx.data_ptr(), lse.data_ptr(),
+              _lib.ptr(sl), _lib.ptr(masks), B, S, H, D, ld, H * D, int(causal), 1.0 / math.sqrt(D), float(p),
+              _lib.stream())
+    return ctx, lse, masks
+
+
+def _attn_bwd_f32(dctx, qkv, ctx, lse, B, S, H, D, causal, slopes, p, masks):
+    dctx = dctx.contiguous()
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+    sl = slopes.to(device=qkv.device, dtype=torch.float32).contiguous() if slopes is not None else None
+    ld, es = 3 * H * D, qkv.element_size()
+    qb, gb = qkv.data_ptr(), dqkv.data_ptr()
+    _lib.call("dtd_attn_bwd_f32", qb, qb + H * D * es, qb + 2 * H * D * es, ctx.data_ptr(), dctx.data_ptr(),
+              lse.data_ptr(), delta.data_ptr(), _lib.ptr(masks if p > 0 else None), gb, gb + H * D * es,
+              gb + 2 * H * D * es, _lib.ptr(sl), B, S, H, D, ld, H * D, int(causal), 1.0 / math.sqrt(D), float(p),
+              _lib.stream())
     return dqkv

@@ -31,6 +31,7 @@
 // loads of the NEXT tile's K-step 0; the epilogue (two rounds of 128 rows through LDS buffer 1,
 // stored as full 512-byte row segments) writes them into buffer 0 meanwhile, so the next tile
 // starts with its first K-step resident.
+#include <stdlib.h>
 #include <type_traits>
 
 #include "common.h"
@@ -79,7 +80,9 @@ __device__ __forceinline__ bf16x4 cvt4(f32x4 v) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3);
 }
 
-template <int EPI>
+// DIAG (timing-only builds, wrong results unless 0): 1 = no barrier in the K loop, 2 = every
+// K-step loads K-step 0 of its tile (L2-hot source), 4 = no staging stores, 8 = no loads in the loop
+template <int EPI, int DIAG = 0>
 __global__ void __launch_bounds__(256, 1) gemm4_kernel(G4Args g) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -107,7 +110,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(G4Args g) {
 
   bf16x8 R[16];
   auto gload = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int kt) {
-    const int ko = kt * BK * 2;
+    const int ko = (DIAG & 2) ? 0 : kt * BK * 2;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
       R[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, voa, i * sta + ko, 0));
@@ -116,6 +119,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(G4Args g) {
       R[8 + i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, vob, i * stb + ko, 0));
   };
   auto swrite = [&](char* buf) {
+    if constexpr ((DIAG & 4) != 0) return;
 #pragma unroll
     for (int i = 0; i < 8; ++i) *reinterpret_cast<bf16x8*>(buf + lst + i * 4096) = R[i];
 #pragma unroll
@@ -189,7 +193,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(G4Args g) {
         __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write
       }
       __builtin_amdgcn_sched_barrier(0);
-      gload(la, lb, lk);
+      if constexpr ((DIAG & 8) == 0) gload(la, lb, lk);
       mma(first_c, I4{}, I8{}, A0, B0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -198,7 +202,7 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(G4Args g) {
       }
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      bar();
+      if constexpr ((DIAG & 1) == 0) bar();
       // ---- phase 1: MFMAs on F1 with the F0 reads of K-step gk + 1
       fread(nxt, ch0, A0, B0);
       mma(std::false_type{}, I0{}, I8{}, A1, B1);
@@ -290,6 +294,14 @@ DTD_EXPORT int dtd_gemm4_bt(int epi, const void* a, int lda, const void* b, int 
   const int ntiles = (M / BM) * (N / BN);
   const int cus = num_cus4() / 8 * 8;
   const int nwg = ntiles >= cus ? cus : (ntiles + 7) / 8 * 8;
-  hipLaunchKernelGGL(gemm4_kernel<E4_STORE>, dim3(nwg), dim3(256), 0, s, g);
+  static const int diag = getenv("DTD_GEMM4_DIAG") ? atoi(getenv("DTD_GEMM4_DIAG")) : 0;
+  switch (diag) {
+    case 1: hipLaunchKernelGGL((gemm4_kernel<E4_STORE, 1>), dim3(nwg), dim3(256), 0, s, g); break;
+    case 2: hipLaunchKernelGGL((gemm4_kernel<E4_STORE, 2>), dim3(nwg), dim3(256), 0, s, g); break;
+    case 4: hipLaunchKernelGGL((gemm4_kernel<E4_STORE, 4>), dim3(nwg), dim3(256), 0, s, g); break;
+    case 8: hipLaunchKernelGGL((gemm4_kernel<E4_STORE, 8>), dim3(nwg), dim3(256), 0, s, g); break;
+    case 15: hipLaunchKernelGGL((gemm4_kernel<E4_STORE, 15>), dim3(nwg), dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((gemm4_kernel<E4_STORE, 0>), dim3(nwg), dim3(256), 0, s, g);
+  }
   DTD_LAUNCH_CHECK();
 }

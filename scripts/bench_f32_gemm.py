@@ -1,0 +1,47 @@
+#!/usr/bin/env python
+"""fp32 GEMM throughput of the vendor library (hipBLASLt / rocBLAS through torch) at the BERT-base
+projection shapes, against the 157 TF/s f32 MFMA peak: decides whether the reference-precision
+path needs a hand-written f32 GEMM (cdna_hip_programming.md §3: an untuned f32-MFMA kernel
+reaches 122 TF/s at 4096^3)."""
+import json
+import os
+import statistics
+
+import torch
+
+
+def timed(fn, reps=5):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+def main():
+    T = int(os.environ.get("T", 32768))
+    H, F = 768, 3072
+    torch.manual_seed(0)
+    x = torch.randn(T, H, device="cuda")
+    xf = torch.randn(T, F, device="cuda")
+    w = {"qkv": torch.randn(3 * H, H, device="cuda"), "o": torch.randn(H, H, device="cuda"),
+         "fc1": torch.randn(F, H, device="cuda"), "fc2": torch.randn(H, F, device="cuda")}
+    L = torch.nn.functional.linear
+    cases = {"fwd_qkv": (x, w["qkv"]), "fwd_o": (x, w["o"]), "fwd_fc1": (x, w["fc1"]), "fwd_fc2": (xf, w["fc2"])}
+    out = {}
+    for k, (a, b) in cases.items():
+        fl = 2 * a.shape[0] * a.shape[1] * b.shape[0]
+        ts = [timed(lambda a=a, b=b: L(a, b)) for _ in range(3)]
+        t = statistics.median(ts)
+        out[k] = {"us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
+        print(json.dumps({k: out[k]}), flush=True)
+    # the same with TF32-like reduced precision explicitly off (torch's default for fp32 matmul)
+    print(json.dumps({"T": T, "allow_tf32": torch.backends.cuda.matmul.allow_tf32, "results": out}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -157,3 +157,28 @@ def test_mask_generator_matches_reference_bits(S):
     ref = attn_keep_mask(B, H, S, p, 21, 0, 6).view(B * H, S, S).to(torch.int64)
     assert torch.equal(a, ref)
     assert torch.equal(b, ref)
+
+
+@pytest.mark.parametrize("B,S,H,D,causal,alibi,p", CASES)
+def test_f32_attention_kernels_match_fp64(B, S, H, D, causal, alibi, p):
+    """Reference-precision path (ops/csrc/attention_f32.hip, exact f32 MFMA products): forward
+    output / LSE and dQ, dK, dV against an fp64 evaluation of the same math (same dropout masks:
+    the kernel takes the bits of the HIP generator, the reference regenerates them bit-identically)."""
+    torch.manual_seed(1)
+    qkv = torch.randn(B * S, 3 * H * D, dtype=torch.float32)
+    dctx = torch.randn(B * S, H * D, dtype=torch.float32)
+    slopes = A.alibi_slopes(H) if alibi else None
+    rg, rc = RngState(13, device="cuda"), RngState(13, device="cpu")
+    assert A.f32_kernel_supported(qkv.cuda(), D)
+    ctx_g, lse_g, mk = A.attn_fwd(qkv.cuda(), B, S, H, D, causal, slopes, p, rg, 5)
+    ctx_r, lse_r = A.attn_fwd_ref(qkv.double(), B, S, H, D, causal, slopes, p, rc, 5)
+    assert ctx_g.dtype == torch.float32
+    assert rel(ctx_g, ctx_r) < 2e-5, rel(ctx_g, ctx_r)
+    assert (lse_g.cpu().double() - lse_r).abs().max().item() < 1e-4
+    dq_g = A.attn_bwd(dctx.cuda(), qkv.cuda(), ctx_g, lse_g, B, S, H, D, causal, slopes, p, rg, 5, mk)
+    dq_r = A.attn_bwd_ref(dctx.double(), qkv.double(), ctx_r, lse_r, B, S, H, D, causal, slopes, p, rc, 5)
+    g = dq_g.view(B, S, 3, H, D).cpu().double()
+    r = dq_r.view(B, S, 3, H, D)
+    for i, name in enumerate("qkv"):
+        e = rel(g[:, :, i], r[:, :, i])
+        assert e < 5e-5, f"d{name} rel err {e}"
