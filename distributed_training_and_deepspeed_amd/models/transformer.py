@@ -85,7 +85,13 @@ def stage_dgrad_transposes(layers, x: torch.Tensor) -> None:
     rt = layers[0].rt
     rt.pending_wt = None
     if layers[0].training and torch.is_grad_enabled() and x.is_cuda and rt.use_fused(x):
-        rt.pending_wt = [w for layer in layers for w in (layer.qkv_w, layer.o_w, layer.fc1_w, layer.fc2_w)]
+        # which W^T the backward will read: every projection's in the NT input-gradient form, else
+        # only fc2's (the fused FFN-backward GEMM, which needs the kept activation)
+        if G.dgrad_nt_enabled():
+            names = ("qkv_w", "o_w", "fc1_w", "fc2_w")
+        else:
+            names = ("fc2_w",) if rt.keep_ffn_act else ()
+        rt.pending_wt = [getattr(layer, n) for layer in layers for n in names] or None
 
 
 def prefetch_masks(layers, input_ids: torch.Tensor) -> None:

@@ -315,11 +315,17 @@ def prepare_transposes(weights) -> None:
 
 
 def transposed(w: torch.Tensor) -> torch.Tensor:
-    """W^T: the copy prepare_transposes made for this backward, else a fresh transpose."""
-    e = _WT_CACHE.get(id(w))
+    """W^T: the copy prepare_transposes made for this backward (handed out once: the entry is
+    dropped, so each copy is freed right after its layer's input-gradient GEMM instead of living
+    until the next forward), else a fresh transpose."""
+    e = _WT_CACHE.pop(id(w), None)
     if e is not None and e[0] is w and e[1] == w.data_ptr():
         return e[2]
     return transpose(w)
+
+
+def dgrad_nt_enabled() -> bool:
+    return _DGRAD_NT[0]
 
 
 def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
