@@ -267,6 +267,195 @@ __global__ void __launch_bounds__(256, 1) gemm4_kernel(G4Args g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ring form (default when K % 128 == 0, K >= 256): the staging registers form a TWO-deep ring, so
+// a K-step's global loads are issued two K-steps (~4k cycles) before their LDS stores -- one
+// K-step of lead (the form above) left the single wave per SIMD waiting on L2 / HBM latency.
+// The registers for the second staging set come from the fragments: B fragments are double
+// buffered per 32-deep slice (2 x 32 VGPRs) and A fragments are streamed one 16-row block ahead
+// (2 x 4 VGPRs) instead of a whole K-step of both (128 VGPRs).  Streaming A means a buffer is read
+// until the end of its K-step, so there are two barriers per K-step: B_j at its start (every wave
+// finished reading K-step j-1's buffer -> K-step j+1 may be stored there) and B'_j in the middle
+// (K-step j+1 stored -> its fragments may be read during slice 1).
+//   K-step j, slice 0: MFMAs on (B0, A streamed) | read A of slice 0, B of slice 1 (buffer j) |
+//                      store ring set (j+1)&1 = K-step j+1, reload it with K-step j+3
+//   B'_j
+//   K-step j, slice 1: MFMAs on (B1, A streamed) | read A of slice 1, then A / B of K-step j+1's
+//                      slice 0 (buffer j+1)
+template <int EPI, int DIAG = 0>
+__global__ void __launch_bounds__(256, 1) gemm4r_kernel(G4Args g) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lq = lane >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn, nk = g.K / BK;
+  const int nwg = gridDim.x, x = blockIdx.x % 8, l = blockIdx.x / 8, per = nwg / 8;
+  const int q = ntiles / 8, r = ntiles % 8;
+  const int beg = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const int end = beg + q + (x < r ? 1 : 0);
+  int t = beg + l;
+  if (t >= end) return;
+  int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+
+  const int srow = tid >> 3, sc = tid & 7;
+  const int lst = srow * 128 + ((sc ^ (srow & 7)) << 4);
+  const int voa = (srow * g.lda + sc * 8) * 2, vob = (srow * g.ldb + sc * 8) * 2;
+  const int sta = 32 * g.lda * 2, stb = 32 * g.ldb * 2;
+  const int fa = (wm * 128 + li) * 128, fb = PANEL + (wn * 128 + li) * 128;
+  const int ch0 = (lq ^ (li & 7)) << 4, ch1 = ((4 + lq) ^ (li & 7)) << 4;
+
+  bf16x8 R0[16], R1[16];
+  // staging piece i of a K-step: i < 8 -> A rows srow + 32 i, else B rows srow + 32 (i - 8)
+  auto gload1 = [&](bf16x8 (&R)[16], int i, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int kt) {
+    const int ko = (DIAG & 2) ? 0 : kt * BK * 2;
+    if (i < 8) R[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, voa, i * sta + ko, 0));
+    else R[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, vob, (i - 8) * stb + ko, 0));
+  };
+  auto swrite1 = [&](const bf16x8 (&R)[16], char* buf, int i) {
+    if constexpr ((DIAG & 4) != 0) return;
+    *reinterpret_cast<bf16x8*>(buf + (i < 8 ? 0 : PANEL) + lst + (i & 7) * 4096) = R[i];
+  };
+  auto rdA = [&](const char* buf, int ch, int mi) { return *reinterpret_cast<const bf16x8*>(buf + fa + mi * 2048 + ch); };
+  auto rdB = [&](const char* buf, int ch, int ni) { return *reinterpret_cast<const bf16x8*>(buf + fb + ni * 2048 + ch); };
+  bf16x8 B0[8], B1[8], A0, A1;
+  f32x4 acc[8][8];
+
+  auto rsa = uniform_rsrc(g.a + (size_t)m0 * g.lda), rsb = uniform_rsrc(g.b + (size_t)n0 * g.ldb);
+  // prologue: K-step 0 in buffer 0, K-steps 1 and 2 in flight in R1 / R0, fragments of K-step 0
+#pragma unroll
+  for (int i = 0; i < 16; ++i) gload1(R0, i, rsa, rsb, 0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) swrite1(R0, smem, i);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) gload1(R1, i, rsa, rsb, 1);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) gload1(R0, i, rsa, rsb, 2);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bar();
+#pragma unroll
+  for (int ni = 0; ni < 8; ++ni) B0[ni] = rdB(smem, ch0, ni);
+  A0 = rdA(smem, ch0, 0);
+
+  while (true) {
+    const int tn = t + per;
+    const bool has_next = tn < end;
+    const int m1 = has_next ? (tn / ntn) * BM : m0, n1 = has_next ? (tn % ntn) * BN : n0;
+    const auto rsa1 = uniform_rsrc(g.a + (size_t)m1 * g.lda), rsb1 = uniform_rsrc(g.b + (size_t)n1 * g.ldb);
+    // K-step j (parity PAR = j & 1, buffers fixed by it since nk is even)
+    auto kstep = [&](auto par_c, auto first_c, int j) {
+      constexpr int PAR = decltype(par_c)::value;
+      constexpr bool FIRST = decltype(first_c)::value;
+      bf16x8 (&Rw)[16] = PAR ? R0 : R1;   // holds K-step j+1 (loaded during j-2)
+      char* cur = smem + PAR * BUF;
+      char* nxt = smem + (PAR ^ 1) * BUF;
+      const bool here = j + 3 < nk;
+      const auto la = here ? rsa : rsa1, lb = here ? rsb : rsb1;
+      const int lk = here ? j + 3 : (has_next ? j + 3 - nk : nk - 1);
+      if constexpr ((DIAG & 1) == 0) bar();                  // B_j
+      // ---- slice 0
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        bf16x8& Ac = (mi & 1) ? A1 : A0;
+        bf16x8& An = (mi & 1) ? A0 : A1;
+        An = mi < 7 ? rdA(cur, ch0, mi + 1) : rdA(cur, ch1, 0);
+        if (mi >= 4) {
+          B1[2 * (mi - 4)] = rdB(cur, ch1, 2 * (mi - 4));
+          B1[2 * (mi - 4) + 1] = rdB(cur, ch1, 2 * (mi - 4) + 1);
+        }
+        swrite1(Rw, nxt, 2 * mi);
+        swrite1(Rw, nxt, 2 * mi + 1);
+        if constexpr ((DIAG & 8) == 0) {
+          gload1(Rw, 2 * mi, la, lb, lk);
+          gload1(Rw, 2 * mi + 1, la, lb, lk);
+        }
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni)
+          acc[mi][ni] = mfma16(B0[ni], Ac, FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mi][ni]);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);   // DS write
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);   // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr ((DIAG & 1) == 0) bar();                  // B'_j
+      // ---- slice 1
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        bf16x8& Ac = (mi & 1) ? A1 : A0;
+        bf16x8& An = (mi & 1) ? A0 : A1;
+        An = mi < 7 ? rdA(cur, ch1, mi + 1) : rdA(nxt, ch0, 0);
+        if (mi >= 4) {
+          B0[2 * (mi - 4)] = rdB(nxt, ch0, 2 * (mi - 4));
+          B0[2 * (mi - 4) + 1] = rdB(nxt, ch0, 2 * (mi - 4) + 1);
+        }
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = mfma16(B1[ni], Ac, acc[mi][ni]);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    kstep(std::integral_constant<int, 0>{}, std::true_type{}, 0);
+    kstep(std::integral_constant<int, 1>{}, std::false_type{}, 1);
+    for (int j = 2; j < nk; j += 2) {
+      kstep(std::integral_constant<int, 0>{}, std::false_type{}, j);
+      kstep(std::integral_constant<int, 1>{}, std::false_type{}, j + 1);
+    }
+
+    // ---- epilogue through buffer 1 (the last K-step's; buffer 0 holds the next tile's K-step 0)
+    f32x4 bv[8];
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+      bv[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (g.bias) {
+        const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n0 + wn * 128 + ni * 16 + 4 * lq);
+        bv[ni] = __builtin_convertvector(b4, f32x4);
+      }
+    }
+    bar();   // every wave is done reading buffer 1
+    char* img = smem + BUF;
+    const int c = lane & 31;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+      for (int m4 = 0; m4 < 4; ++m4) {
+        const int mi = rr * 4 + m4;
+        const int ir = wm * 64 + m4 * 16 + li;
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+          const int n = wn * 128 + ni * 16 + 4 * lq;
+          *reinterpret_cast<bf16x4*>(img + ir * 512 + (((n >> 2) ^ ((ir & 15) << 1)) << 3)) =
+              cvt4(acc[mi][ni] + bv[ni]);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ir = w * 32 + 2 * i + (lane >> 5);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + ir * 512 + ((c ^ (ir & 15)) << 4));
+        const int tr = (ir >> 6) * 128 + rr * 64 + (ir & 63);
+        *reinterpret_cast<bf16x8*>(g.c + (size_t)(m0 + tr) * g.ldc + n0 + c * 8) = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+    }
+    if (!has_next) break;
+    t = tn;
+    m0 = m1;
+    n0 = n1;
+    rsa = rsa1;
+    rsb = rsb1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 int num_cus4() {
   static int n = 0;
   if (n == 0) {
@@ -295,6 +484,18 @@ DTD_EXPORT int dtd_gemm4_bt(int epi, const void* a, int lda, const void* b, int 
   const int cus = num_cus4() / 8 * 8;
   const int nwg = ntiles >= cus ? cus : (ntiles + 7) / 8 * 8;
   static const int diag = getenv("DTD_GEMM4_DIAG") ? atoi(getenv("DTD_GEMM4_DIAG")) : 0;
+  static const int form = getenv("DTD_GEMM4_FORM") ? atoi(getenv("DTD_GEMM4_FORM")) : 1;
+  if (form == 1 && K % (2 * BK) == 0 && K >= 4 * BK) {
+    switch (diag) {
+      case 1: hipLaunchKernelGGL((gemm4r_kernel<E4_STORE, 1>), dim3(nwg), dim3(256), 0, s, g); break;
+      case 2: hipLaunchKernelGGL((gemm4r_kernel<E4_STORE, 2>), dim3(nwg), dim3(256), 0, s, g); break;
+      case 4: hipLaunchKernelGGL((gemm4r_kernel<E4_STORE, 4>), dim3(nwg), dim3(256), 0, s, g); break;
+      case 8: hipLaunchKernelGGL((gemm4r_kernel<E4_STORE, 8>), dim3(nwg), dim3(256), 0, s, g); break;
+      case 15: hipLaunchKernelGGL((gemm4r_kernel<E4_STORE, 15>), dim3(nwg), dim3(256), 0, s, g); break;
+      default: hipLaunchKernelGGL((gemm4r_kernel<E4_STORE, 0>), dim3(nwg), dim3(256), 0, s, g);
+    }
+    DTD_LAUNCH_CHECK();
+  }
   switch (diag) {
     case 1: hipLaunchKernelGGL((gemm4_kernel<E4_STORE, 1>), dim3(nwg), dim3(256), 0, s, g); break;
     case 2: hipLaunchKernelGGL((gemm4_kernel<E4_STORE, 2>), dim3(nwg), dim3(256), 0, s, g); break;

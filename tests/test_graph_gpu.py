@@ -129,3 +129,63 @@ def test_zero_script_graph_captures_bert_mlm_head():
     d = json.loads(line)
     assert d["hip_graph"] is True and d["stage"] == 2
     assert d["final_loss"] == d["final_loss"]   # finite (not NaN)
+
+
+@pytest.mark.parametrize("engine", ["ddp", "zero2", "zero3"])
+def test_captured_step_with_rccl_collectives_matches_eager(engine):
+    """The N > 1 data path inside a hipGraph: force_collectives makes DDP issue its bucket
+    all-reduces (RCCL, from the autograd thread, on RCCL's stream) and ZeRO its reduce-scatters and
+    all-gathers at world 1; the captured step (collectives included) replays exactly like the eager
+    one.  rocprofv3 of bench.py --force-collectives shows the RCCL kernels in the step."""
+    import os
+    from distributed_training_and_deepspeed_amd import comm
+    from distributed_training_and_deepspeed_amd.parallel.zero import initialize
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(32000 + os.getpid() % 1000 + len(engine))
+    comm.init(rank=0, world_size=1, backend="nccl", local_rank=0)
+    try:
+        def setup():
+            if engine == "ddp":
+                model = build_model("tiny", dtype=torch.bfloat16, device="cuda", seed=3)
+                model.rt.mlm_capacity = mlm_capacity(4 * 128)
+                model.rt.mlm_overflow = torch.zeros((), dtype=torch.bool, device="cuda")
+                ddp = DistributedDataParallel(model, bucket_cap_mb=0.25, force_collectives=True)
+                assert ddp.collectives and len(ddp.buckets) > 2
+                opt = hf_adamw(ddp.parameters(), lr=1e-3)
+
+                def step(input_ids, labels):
+                    out = ddp(input_ids, labels=labels)
+                    out.loss.backward()
+                    opt.step()
+                    model.rt.rng.advance()
+                    return out.loss.detach()
+                return model, step
+            model = build_model("causal-tiny", dtype=torch.bfloat16, device="cuda", seed=3)
+            cfg = {"optimizer": {"type": "Adam", "params": {"lr": 1e-3}},
+                   "zero_optimization": {"stage": int(engine[-1]), "reduce_bucket_size": 100000,
+                                         "world1_replicated": False, "force_collectives": True}}
+            eng, _, _, _ = initialize(model=model, model_parameters=model.parameters(), config=cfg)
+            assert eng.collect
+
+            def step(input_ids, labels):
+                out = eng(input_ids, labels=labels)
+                eng.backward(out.loss)
+                eng.step()
+                return out.loss.detach()
+            return model, step
+
+        mlm = engine == "ddp"
+        cfg = build_model("tiny" if mlm else "causal-tiny").cfg
+        ds = SyntheticLMDataset(cfg, 4 * 8, seq_len=128, mlm=mlm, seed=5)
+        ids = ds.input_ids.view(8, 4, 128).cuda()
+        lab = ds.labels.view(8, 4, 128).cuda()
+        ma, sa = setup()
+        mb, sb = setup()
+        cap = CapturedStep(sb, {"input_ids": ids[0], "labels": lab[0]}, warmup=3, runtime=mb.rt)
+        la = [sa(ids[0], lab[0]) for _ in range(3)]
+        la += [sa(ids[i], lab[i]) for i in range(1, 6)]
+        lb = [cap(input_ids=ids[i], labels=lab[i]).clone() for i in range(1, 6)]
+        torch.cuda.synchronize()
+        assert torch.equal(torch.stack(la[3:]), torch.stack(lb)), (la[3:], lb)
+    finally:
+        comm.destroy()
