@@ -235,7 +235,11 @@ def all_gather_coalesced(outputs, inputs, group=None, async_op=False):
     nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
 
     def fn(a):
-        if nccl and len(outputs) > 1:
+        # one RCCL group launch -- except inside a hipGraph capture, where torch's coalescing
+        # manager is not capturable (the capture's end-of-capture crashed in it): there each
+        # gather is its own captured RCCL call
+        capturing = outputs and outputs[0].is_cuda and torch.cuda.is_current_stream_capturing()
+        if nccl and len(outputs) > 1 and not capturing:
             with dist._coalescing_manager(group=group, device=outputs[0].device, async_ops=True) as cm:
                 for o, i in zip(outputs, inputs):
                     dist.all_gather_into_tensor(o, i, group=group)

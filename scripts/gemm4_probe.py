@@ -26,13 +26,13 @@ for n, ww in w.items():
     ts = [timed(lambda: G.gemm4_bt(x, ww)) for _ in range(5)]
     hb = [timed(lambda: torch.nn.functional.linear(x, ww)) for _ in range(5)]
     out[n] = {"gemm4_us": round(statistics.median(ts), 1), "hipblaslt_us": round(statistics.median(hb), 1)}
-print(json.dumps({"diag": int(os.environ.get("DTD_GEMM4_DIAG", "0")), **out}), flush=True)
+print(json.dumps({"form": int(os.environ.get("DTD_GEMM4_FORM", "1")), "diag": int(os.environ.get("DTD_GEMM4_DIAG", "0")), **out}), flush=True)
 '''
 
-for d in (0, 1, 2, 4, 8, 15):
-    env = dict(os.environ, DTD_GEMM4_DIAG=str(d))
+for form, d in ((0, 0), (1, 0), (0, 1), (0, 2), (0, 4), (0, 8), (0, 15), (1, 1), (1, 2), (1, 4), (1, 8), (1, 15)):
+    env = dict(os.environ, DTD_GEMM4_DIAG=str(d), DTD_GEMM4_FORM=str(form))
     r = subprocess.run([sys.executable, "-c", CODE], env=env, capture_output=True, text=True, timeout=240)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    print(line[-1] if line else json.dumps({"diag": d, "error": r.stderr[-500:]}), flush=True)
+    print(line[-1] if line else json.dumps({"form": form, "diag": d, "error": r.stderr[-500:]}), flush=True)
     if r.returncode != 0:
         sys.exit(r.returncode)

@@ -166,9 +166,16 @@ def test_zero_two_ranks_share_one_gpu_match_stage0(tmp_path, free_port, stage):
 
     p0, ps = res[0][0]["params"], res[stage][0]["params"]
     assert p0.keys() == ps.keys()
+    # compare the training UPDATES (final - initial): Adam moves every element by up to ~lr per step
+    # whatever its gradient's size, so elements whose tiny gradients differ by reduction order can
+    # flip direction -- bound each element by 2 lr per step and the update's relative norm by 5 %
+    init = {n: p.detach().to(torch.bfloat16).float() for n, p in build_model("causal-tiny", seed=3).named_parameters()}
     for n in p0:
         assert torch.isfinite(ps[n]).all(), n
-        assert (p0[n] - ps[n]).abs().max().item() < 2e-3, (stage, n, (p0[n] - ps[n]).abs().max().item())
+        d0, ds = p0[n] - init[n], ps[n] - init[n]
+        assert (d0 - ds).abs().max().item() <= 2 * 1e-3 * 3 + 1e-4, (stage, n, (d0 - ds).abs().max().item())
+        rel = ((d0 - ds).norm() / (d0.norm() + 1e-12)).item()
+        assert rel < 0.05, (stage, n, rel)
 
 
 def test_rccl_bf16_avg_collectives_used_by_ddp_and_zero(rccl_world1):
