@@ -85,6 +85,11 @@ _SIGS = {
     # gemm4.hip
     "dtd_gemm4_supported": (I, [I, I, I]),
     "dtd_gemm4_bt": (I, [I, P, I, P, I, P, I, P, I, I, I, P]),
+    # gemm_f32.hip
+    "dtd_gemm_f32_supported": (I, [I, I, I]),
+    "dtd_gemm_f32_nt": (I, [P, I, P, I, P, I, P, I, I, I, P]),
+    "dtd_gemm_f32_tn_splits": (I, [I, I, I]),
+    "dtd_gemm_f32_tn": (I, [P, I, P, I, P, I, I, I, I, P]),
     # reduce.hip
     "dtd_splitk_reduce": (I, [P, I, I, ctypes.c_longlong, P, I, I, P]),
 }

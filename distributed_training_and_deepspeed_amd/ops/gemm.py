@@ -105,8 +105,54 @@ def set_all(on: bool) -> None:
     _ALL[0] = bool(on)
 
 
+# fp32 (reference-precision) products on the hand-written f32-MFMA kernel (ops/csrc/gemm_f32.hip):
+# forward, NT input gradient and split-K weight gradient (DTD_GEMM_F32=1; default off until measured).
+_F32 = [os.environ.get("DTD_GEMM_F32", "0") == "1"]
+
+
+def set_f32(on: bool) -> None:
+    _F32[0] = bool(on)
+
+
+def _ok32(t: torch.Tensor) -> bool:
+    return (t is not None and t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+            and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0)
+
+
+def f32_supported(M: int, N: int, K: int, *tensors) -> bool:
+    if not (_F32[0] and all(_ok32(t) for t in tensors) and _lib.has("dtd_gemm_f32_nt")):
+        return False
+    return bool(_lib.lib().dtd_gemm_f32_supported(M, N, K))
+
+
+def gemm_f32_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """a . b^T (+ bias), fp32, exact f32 MFMA products."""
+    M, K = a.shape
+    N = b.shape[0]
+    c = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    _lib.call("dtd_gemm_f32_nt", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+              _lib.ptr(bias), M, N, K, _lib.stream())
+    return c
+
+
+def gemm_f32_tn(a: torch.Tensor, b: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+    """fp32 partials [splits, M, N] of a^T b (a [K, M], b [K, N]) over contiguous K ranges."""
+    K, M = a.shape
+    N = b.shape[1]
+    if splits is None:
+        splits = _lib.lib().dtd_gemm_f32_tn_splits(M, N, K)
+    part = torch.empty((splits, M, N), dtype=torch.float32, device=a.device)
+    _lib.call("dtd_gemm_f32_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), part.data_ptr(), M, N, K,
+              splits, _lib.stream())
+    return part
+
+
 def linear_any(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
-    """F.linear, or the hand-written kernel in the all-native mode when the shape tiles."""
+    """F.linear, or a hand-written kernel: the fp32 one for fp32 operands, the bf16 one in the
+    all-native mode, when the shape tiles."""
+    if (x.dtype == torch.float32 and x.dim() == 2 and f32_supported(x.shape[0], w.shape[0], x.shape[1], x, w)
+            and (b is None or _ok1d32(b))):
+        return gemm_f32_nt(x, w, b)
     if all_enabled() and x.dim() == 2 and supported(x.shape[0], w.shape[0], x.shape[1], x, w) and (
             b is None or (b.is_cuda and b.dtype == torch.bfloat16 and b.is_contiguous())):
         return linear(x, w, b)
@@ -328,9 +374,23 @@ def dgrad_nt_enabled() -> bool:
     return _DGRAD_NT[0]
 
 
+def _ok1d32(t: torch.Tensor) -> bool:
+    return t.is_cuda and t.dtype == torch.float32 and t.dim() == 1 and t.is_contiguous() and t.data_ptr() % 16 == 0
+
+
+def _t32(w: torch.Tensor) -> torch.Tensor:
+    """W^T of an fp32 weight (contiguous), cached for this backward like the bf16 copies."""
+    e = _WT_CACHE.pop(id(w), None)
+    if e is not None and e[0] is w and e[1] == w.data_ptr():
+        return e[2]
+    return w.t().contiguous()
+
+
 def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dy @ w for a Linear weight w [out, in], through the NT form when it applies (the
-    hand-written kernel in the all-native mode)."""
+    hand-written kernel in the all-native mode; the fp32 kernel for fp32 operands)."""
+    if dy.dtype == torch.float32 and dy.dim() == 2 and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w):
+        return gemm_f32_nt(dy, _t32(w))
     wt = transposed_for_dgrad(w)
     if wt is None:
         return dy @ w
@@ -341,6 +401,8 @@ def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 def dgrad_add_(c: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """c += dy @ w in place (residual-branch input gradient), NT form when it applies."""
+    if dy.dtype == torch.float32 and dy.dim() == 2 and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w, c):
+        return c.add_(gemm_f32_nt(dy, _t32(w)))
     wt = transposed_for_dgrad(w)
     if wt is None:
         return c.addmm_(dy, w)

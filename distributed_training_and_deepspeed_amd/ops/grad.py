@@ -193,6 +193,12 @@ def _emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
     dst, acc = grad_dst(p)
     T, o = dy.shape
     i = x.shape[1]
+    if dy.is_cuda and dy.dtype == torch.float32:
+        from . import gemm as G
+        if G.f32_supported(o, i, T, dy, x):
+            # reference-precision path: the f32-MFMA TN kernel, fp32 split-K partials
+            splitk_reduce(G.gemm_f32_tn(dy, x), dst, acc)
+            return
     if dy.is_cuda and T >= 8192:
         from . import gemm as G
         if G.wgrad_enabled() and G.wgrad_preferred(o, i) and G.wgrad_supported(dy, x):
