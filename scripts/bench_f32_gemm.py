@@ -39,6 +39,23 @@ def main():
         t = statistics.median(ts)
         out[k] = {"us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
         print(json.dumps({k: out[k]}), flush=True)
+    # the hand-written f32-MFMA kernel (ops/csrc/gemm_f32.hip): NT forward and split-K TN wgrad
+    from distributed_training_and_deepspeed_amd.ops import gemm as G
+    G.set_f32(True)
+    for k, (a, b) in cases.items():
+        fl = 2 * a.shape[0] * a.shape[1] * b.shape[0]
+        t = statistics.median([timed(lambda a=a, b=b: G.gemm_f32_nt(a, b)) for _ in range(3)])
+        out["hand_" + k] = {"us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
+        print(json.dumps({"hand_" + k: out["hand_" + k]}), flush=True)
+    dy = {"qkv": torch.randn(T, 3 * H, device="cuda"), "o": x, "fc1": torch.randn(T, F, device="cuda"), "fc2": x}
+    xin = {"qkv": x, "o": x, "fc1": x, "fc2": xf}
+    for k in ("qkv", "o", "fc1", "fc2"):
+        fl = 2 * T * dy[k].shape[1] * xin[k].shape[1]
+        t = statistics.median([timed(lambda k=k: dy[k].t() @ xin[k]) for _ in range(3)])
+        out["wgrad_" + k] = {"us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
+        t = statistics.median([timed(lambda k=k: G.gemm_f32_tn(dy[k], xin[k]).sum(0)) for _ in range(3)])
+        out["hand_wgrad_" + k] = {"us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
+        print(json.dumps({k: [out["wgrad_" + k], out["hand_wgrad_" + k]]}), flush=True)
     # the same with TF32-like reduced precision explicitly off (torch's default for fp32 matmul)
     print(json.dumps({"T": T, "allow_tf32": torch.backends.cuda.matmul.allow_tf32, "results": out}), flush=True)
 
