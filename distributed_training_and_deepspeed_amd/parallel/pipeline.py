@@ -59,6 +59,9 @@ class IdleTimeTracker:
         self.device_idle_time = {i: (0.0, 0) for i in range(len(self.devices))}
         self._last = {}
         self._pending = []
+        # off while a step is captured into / replayed from a hipGraph: an event recorded during
+        # capture is only a dependency marker, not a timestamp
+        self.enabled = True
 
     def _stamp(self, idx: int):
         if self.timing == "host":
@@ -68,6 +71,8 @@ class IdleTimeTracker:
         return ev
 
     def mark(self, idx: int, forward: bool, entering: bool) -> None:
+        if not self.enabled:
+            return
         now = self._stamp(idx)
         last = self._last.get(idx)
         msg = f"{'Entering' if entering else 'Finished'} {'forward' if forward else 'backward'} pass on device {idx}"

@@ -131,6 +131,30 @@ def test_zero_script_graph_captures_bert_mlm_head():
     assert d["final_loss"] == d["final_loss"]   # finite (not NaN)
 
 
+@pytest.mark.parametrize("mode", ["naive", "gpipe", "1f1b"])
+def test_mp_script_graph_trains_like_eager(mode):
+    """model_parallel_training.py with two virtual stages on one GPU: --graph (the whole step --
+    every micro-batch forward/backward of both stages, loss, per-device optimizer, RNG advance --
+    as one hipGraph) trains the same steps on the same batches as the eager issue."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    extra = [] if mode == "naive" else ["--pipeline", "--schedule", mode, "--checkpoint", "never"]
+    for g in ("off", "on"):
+        r = subprocess.run([sys.executable, os.path.join(root, "model_parallel_training.py"), "--model", "bert-tiny",
+                            "--devices", "cuda:0,cuda:0", "--batch-size", "8", "--micro-batch-count", "4",
+                            "--training-steps", "8", "--seq-len", "128", "--graph", g] + extra,
+                           cwd=root, capture_output=True, text=True, timeout=150)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[g] = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["on"]["graph"] and not res["off"]["graph"]
+    a, b = res["off"]["final_loss"], res["on"]["final_loss"]
+    assert abs(a - b) <= 1e-3 * abs(a), (a, b)
+
+
 @pytest.mark.parametrize("engine", ["ddp", "zero2", "zero3"])
 def test_captured_step_with_rccl_collectives_matches_eager(engine):
     """The N > 1 data path inside a hipGraph: force_collectives makes DDP issue its bucket
