@@ -65,6 +65,7 @@ _SIGS = {
     "dtd_attn_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, U32, P]),
     "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, P]),
     "dtd_attn_masks": (I, [P, I, I, I, F, P, U32, P]),
+    "dtd_attn_set_bwd_form": (I, [I]),
     # attention_f32.hip
     "dtd_attn_fwd_f32": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
     "dtd_attn_bwd_f32": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),

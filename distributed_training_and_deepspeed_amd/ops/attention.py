@@ -110,6 +110,18 @@ def _warn_once():
         _WARNED.append(1)
 
 
+def set_bwd_form(form: str) -> str:
+    """'fused': one-kernel backward (attn_bwd_fused_kernel: one workgroup per (batch, head), dQ
+    reduced in LDS) where it applies -- head_dim 64, no causal mask / ALiBi, S % 128 == 0, S <= 512;
+    'split': the dQ + dK/dV kernel pair.  Returns the previous form."""
+    old = _lib.lib().dtd_attn_set_bwd_form(1 if form == "fused" else 0)
+    return "fused" if old else "split"
+
+
+def fused_bwd_applies(S: int, D: int, causal: bool, slopes) -> bool:
+    return D == 64 and not causal and slopes is None and S % 128 == 0 and S <= 512
+
+
 def kernel_supported(qkv: torch.Tensor, D: int) -> bool:
     return qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128) and _lib.has("dtd_attn_fwd")
 

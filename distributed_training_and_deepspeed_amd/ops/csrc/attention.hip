@@ -1256,6 +1256,286 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused backward (D = 64, no causal mask, no ALiBi, S = 128 NKB <= 512): ONE workgroup per
+// (batch, head) owns every key, so dQ needs neither atomics nor a second kernel that recomputes
+// the softmax.  Five MFMA products per score tile instead of the split kernels' seven, and the
+// per-score VALU work (exp, dropout select, dS) done once instead of twice.
+//   * wave w keeps dK^T / dV^T of its KPW = S/4 keys in accumulator registers (key on the lane,
+//     as in attn_bwd_dkdv_kernel: 256 of the 512 registers at S = 512); the whole K and V of the
+//     head sit in LDS (swizzled 128-byte rows): row reads for S and dP, transposed reads of K for dQ;
+//   * the workgroup sweeps 32-row query tiles.  Per round of KH key blocks per wave: S, dP ->
+//     P, dS per 32-key block; dV^T += dO^T.P, dK^T += Q^T.dS; dS^T goes to LDS as a
+//     [key][query] image; barrier; dQ^T (64 x 32) += K^T . dS^T over the round's keys with
+//     16x16x32 MFMAs (wave w: head dims 16w .. 16w+15 of both 16-query halves -- no partial
+//     sums across waves); barrier.  After the last round each wave stores its dQ slice (and its
+//     qkv-bias column sums) and the next tile is staged.
+//   * delta = rowsum(dO * O) of the next tile is formed while it is staged (no separate pass).
+// LDS 154 KiB at S = 512: one workgroup per CU, one wave per SIMD.
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// dK^T / dV^T update with the accumulator pinned to the accumulator file ("+a"): at 256 live
+// accumulator registers the compiler kept some of them in arch VGPRs and copied them into and out
+// of AGPRs around every MFMA (and spilled).  s_nop 1: the A / B operands may be fresh VALU results
+// (cdna_hip_programming.md §5.7 item 2); the accumulate chain itself needs no wait states.
+__device__ __forceinline__ void mfma32_a(f32x16& acc, bf16x8 a, bf16x8 b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// S / dP products with the accumulator in arch VGPRs ("v": the builtin put them in the accumulator
+// file, which the dK/dV accumulators fill, and every softmax read then cost a v_accvgpr_read).
+// C = 0 for the first product of a chain; mfma_vgpr_wait() (12 wait states, 8-pass XDL) before
+// the VALU reads the chain's result.
+__device__ __forceinline__ void mfma32_v0(f32x16& acc, bf16x8 a, bf16x8 b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma32_v(f32x16& acc, bf16x8 a, bf16x8 b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_vgpr_wait(f32x16& x, f32x16& y) {
+  asm volatile("s_nop 11" : "+v"(x), "+v"(y));
+}
+// dQ^T 16x16x32 products, accumulator in arch VGPRs for the same reason (4-pass XDL: the
+// s_nop 7 statement after the chain covers the result's readers)
+__device__ __forceinline__ void mfma16_v(f32x4& acc, bf16x8 a, bf16x8 b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+
+template <int NKB, bool DROP>
+__global__ void __launch_bounds__(256, 1) attn_bwd_fused_kernel(BwdArgs a) {
+  constexpr int D = 64, NC = 4, NDB = 2, SK = 128 * NKB, KPW = 32 * NKB, NT = SK / 32;
+  constexpr int KH = NKB % 2 == 0 ? 2 : 1, NH = NKB / KH;   // key blocks per round, rounds per tile
+  constexpr int DSP = 36;                                   // dS^T image pitch (bf16): 72-byte rows
+  constexpr int DSR = 4 * KH * 32;                          // dS^T image rows (keys of one round)
+  struct Smem {
+    float lse_s[32], del_s[32];
+    bf16 Qs[32 * 64];
+    bf16 Os[32 * 64];
+    bf16 DS[DSR * DSP];
+    bf16 Ks[SK * 64];
+    bf16 Vs[SK * 64];
+  };
+  __shared__ __attribute__((aligned(16))) Smem sm;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5,
+            r = lane & 31;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int S = a.S;   // == SK (host-checked)
+  const float sc2 = a.scale * kLog2e;
+  const float inv_keep = DROP ? 1.f / (1.f - a.p) : 1.f;
+  const int kw0 = w * KPW;
+  const int Sp = 32 * a.W;
+  const float* lseb = a.lse + (size_t)bh * S;
+  const RowSrc qsrc = row_src<D>(a.q + (size_t)b * S * a.ld + h * D, a.ld, S);
+  const RowSrc dsrc = row_src<D>(a.dout + (size_t)b * S * a.ldo + h * D, a.ldo, S);
+  const RowSrc osrc = row_src<D>(a.o + (size_t)b * S * a.ldo + h * D, a.ldo, S);
+  {
+    const RowSrc ksrc = row_src<D>(a.k + (size_t)b * S * a.ld + h * D, a.ld, S);
+    const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {   // 64 rows per thread-round x 2 operands, in 2 passes
+      TileLoader<D, SK / 2> kl, vl;
+      kl.load(ksrc, half * (SK / 2));
+      vl.load(vsrc, half * (SK / 2));
+      kl.store_swz(sm.Ks + half * (SK / 2) * 64);
+      vl.store_swz(sm.Vs + half * (SK / 2) * 64);
+    }
+  }
+  // query-tile staging: Q / dO rows (swizzled), -lse*log2e and -delta of the 32 rows
+  TileLoader<D, 32> ql, dl, ol;
+  float lse_n = 0.f;
+  auto fetch = [&](int q0) {
+    ql.load(qsrc, q0);
+    dl.load(dsrc, q0);
+    ol.load(osrc, q0);
+    if (tid < 32) lse_n = lseb[q0 + tid];
+  };
+  auto stage = [&]() {
+    // thread tid holds row tid >> 3, columns 8 (tid & 7) .. +7 of dO and O
+    float part = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part = fmaf((float)dl.reg[0][j], (float)ol.reg[0][j], part);
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    part += __shfl_xor(part, 4, 64);
+    ql.store_swz(sm.Qs);
+    dl.store_swz(sm.Os);
+    if ((tid & 7) == 0) sm.del_s[tid >> 3] = -part;
+    if (tid < 32) sm.lse_s[tid] = -lse_n * kLog2e;
+  };
+  fetch(0);
+  stage();
+
+  f32x16 dk[NKB][NDB], dv[NKB][NDB];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int d = 0; d < NDB; ++d) { dk[kb][d] = f32x16{}; dv[kb][d] = f32x16{}; }
+  // dQ operand addressing (16x16x32 transposed reads): lane group g16 = lane >> 4 takes keys
+  // 8 g16 .. +7 of a 32-key step; lane 4 qq + pp of the group addresses row 8 g16 + qq (+4)
+  const int g16 = lane >> 4, l16 = lane & 15, qq = l16 >> 2, pp = l16 & 3;
+  const int kcol = 16 * w + 4 * pp;   // K^T rows of this wave: head dims 16w .. 16w+15
+  __syncthreads();
+
+  for (int t = 0; t < NT; ++t) {
+    const int q0 = t * 32;
+    if (t + 1 < NT) fetch(q0 + 32);
+    f32x4 dq2[2] = {f32x4{}, f32x4{}};
+#pragma unroll
+    for (int hf = 0; hf < NH; ++hf) {
+#pragma unroll
+      for (int kk = 0; kk < KH; ++kk) {
+        const int kb = hf * KH + kk;
+        const int key0 = kw0 + 32 * kb;
+        f32x16 sacc, pacc;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          // Q / dO row fragments re-read per key block (LDS bandwidth to spare; registers not)
+          const bf16x8 qa = swz_row_read(sm.Qs, 0, r, 2 * c + hh), kr = swz_row_read(sm.Ks, key0, r, 2 * c + hh);
+          const bf16x8 oa = swz_row_read(sm.Os, 0, r, 2 * c + hh), vr = swz_row_read(sm.Vs, key0, r, 2 * c + hh);
+          if (c == 0) { mfma32_v0(sacc, qa, kr); mfma32_v0(pacc, oa, vr); }
+          else { mfma32_v(sacc, qa, kr); mfma32_v(pacc, oa, vr); }
+        }
+        mfma_vgpr_wait(sacc, pacc);
+        uint64_t mk[16];
+        if constexpr (DROP) {
+          const cu64* mp = (const cu64*)(uintptr_t)(a.maskA + ((size_t)bh * a.W + (w * NKB + kb)) * Sp + q0);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) mk[i] = mp[i];
+        }
+        // -lse*log2e / -delta of this lane's 16 accumulator rows (rows 8g + 4hh + 0..3)
+        f32x4 L4[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) L4[g] = *reinterpret_cast<const f32x4*>(&sm.lse_s[8 * g + 4 * hh]);
+        const f32x2 sc2v = pk2(sc2, sc2);
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          const f32x2 x = pk_fma(pk2(sacc[i], sacc[i + 1]), sc2v, pk2(L4[i >> 2][i & 3], L4[i >> 2][(i & 3) + 1]));
+          sacc[i] = fexp2(x.x);
+          sacc[i + 1] = fexp2(x.y);
+        }
+        f32x4 D4[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) D4[g] = *reinterpret_cast<const f32x4*>(&sm.del_s[8 * g + 4 * hh]);
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          const f32x2 nd = pk2(D4[i >> 2][i & 3], D4[i >> 2][(i & 3) + 1]);
+          if constexpr (DROP) {
+            const f32x2 tt = pk_fma(pk2(sel_keep(pacc[i], mk[i]), sel_keep(pacc[i + 1], mk[i + 1])),
+                                    pk2(inv_keep, inv_keep), nd);
+            const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * tt;                 // dS
+            pacc[i] = ds.x;
+            pacc[i + 1] = ds.y;
+            sacc[i] = sel_keep(sacc[i], mk[i]);                              // P*mask (dV)
+            sacc[i + 1] = sel_keep(sacc[i + 1], mk[i + 1]);
+          } else {
+            const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * (pk2(pacc[i], pacc[i + 1]) + nd);
+            pacc[i] = ds.x;
+            pacc[i + 1] = ds.y;
+          }
+        }
+        bf16* dsrow = sm.DS + ((w * KH + kk) * 32 + r) * DSP + 4 * hh;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 pb, sb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { pb[j] = (bf16)sacc[8 * s2 + j]; sb[j] = (bf16)pacc[8 * s2 + j]; }
+#pragma unroll
+          for (int d = 0; d < NDB; ++d) {
+            mfma32_a(dv[kb][d], tr_operand_swz(sm.Os, 16 * s2, d * 32, lane), pb);
+            mfma32_a(dk[kb][d], tr_operand_swz(sm.Qs, 16 * s2, d * 32, lane), sb);
+          }
+          // dS^T image: registers 8 s2 + 4 jj .. +3 are queries 8 (2 s2 + jj) + 4 hh + 0..3
+          *reinterpret_cast<bf16x4*>(dsrow + 16 * s2) = __builtin_shufflevector(sb, sb, 0, 1, 2, 3);
+          *reinterpret_cast<bf16x4*>(dsrow + 16 * s2 + 8) = __builtin_shufflevector(sb, sb, 4, 5, 6, 7);
+        }
+        // one key block's live range at a time: the dK/dV accumulators take half the register file
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();   // the round's dS^T image complete
+      // dQ^T rows 16w .. 16w+15 x the tile's 32 queries over the round's 4 KH 32 keys
+#pragma unroll 2
+      for (int k0 = 0; k0 < DSR; k0 += 32) {
+        const int key = (k0 / (KH * 32)) * KPW + hf * KH * 32 + (k0 % (KH * 32)) + 8 * g16 + qq;
+        const bf16* ka = sm.Ks + key * 64 + 8 * ((kcol >> 3) ^ swz64(key)) + (kcol & 7);
+        const bf16* kb4 = sm.Ks + (key + 4) * 64 + 8 * ((kcol >> 3) ^ swz64(key + 4)) + (kcol & 7);
+        const bf16x8 A = cat(tr_read(ka), tr_read(kb4));
+        const int lr = k0 + 8 * g16 + qq;
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const bf16* dp = sm.DS + lr * DSP + 16 * qh + 4 * pp;
+          mfma16_v(dq2[qh], A, cat(tr_read(dp), tr_read(dp + 4 * DSP)));
+        }
+      }
+      asm volatile("s_nop 7" : "+v"(dq2[0]), "+v"(dq2[1]));
+      if (hf == NH - 1 && t + 1 < NT) stage();
+      __syncthreads();   // the image consumed (and, after the last round, the next tile staged)
+    }
+    // lane: query q0 + 16 qh + l16, head dims 16w + 4 g16 + 0..3
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      bf16x4 v4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v4[j] = (bf16)(dq2[qh][j] * a.scale);
+        cs[j] += (float)v4[j];
+      }
+      *reinterpret_cast<bf16x4*>(a.dq + (size_t)(b * S + q0 + 16 * qh + l16) * a.ld + h * D + 16 * w + 4 * g16) = v4;
+    }
+    if (a.bias_part) {
+      // column sums over the tile's 32 queries: the 16 lanes of a group x both halves
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cs[j] += __shfl_xor(cs[j], 1, 64);
+        cs[j] += __shfl_xor(cs[j], 2, 64);
+        cs[j] += __shfl_xor(cs[j], 4, 64);
+        cs[j] += __shfl_xor(cs[j], 8, 64);
+      }
+      if (l16 == 0)
+        *reinterpret_cast<f32x4*>(a.bias_part + ((size_t)b * (S / 32) + t) * (3 * a.H * D) + h * D + 16 * w + 4 * g16) =
+            f32x4{cs[0], cs[1], cs[2], cs[3]};
+    }
+  }
+  // the last asm MFMAs' results: 8-pass XDL -> 12 wait states before any other reader
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+    asm volatile("s_nop 11" : "+a"(dk[kb][0]), "+a"(dk[kb][1]), "+a"(dv[kb][0]), "+a"(dv[kb][1]));
+  const float dv_scale = inv_keep;   // the dropped P fed to dV carried keep bits only
+  // epilogue one accumulator tile at a time (the sched barriers keep the compiler from
+  // interleaving them, whose pressure made it spill the dK/dV accumulators inside the main loop)
+  auto put = [&](const f32x16 (&acc)[NDB], float sc, bf16* dst, int colbase, int kb) {
+    if (a.bias_part) {
+      float vk[32];
+#pragma unroll
+      for (int d = 0; d < NDB; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) vk[16 * d + i] = (float)(bf16)(acc[d][i] * sc);
+      const float sk = colsum32(vk, r);
+      a.bias_part[((size_t)b * (S / 32) + w * NKB + kb) * (3 * a.H * D) + colbase + h * D + colsum_col(r, hh)] = sk;
+    }
+    bf16* p = dst + (size_t)(b * S + kw0 + 32 * kb + r) * a.ld + h * D;
+#pragma unroll
+    for (int d = 0; d < NDB; ++d)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        bf16x4 k4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k4[j] = (bf16)(acc[d][4 * gq + j] * sc);
+        *reinterpret_cast<bf16x4*>(p + d * 32 + 8 * gq + 4 * hh) = k4;
+      }
+  };
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    put(dk[kb], a.scale, a.dk, a.H * D, kb);
+    __builtin_amdgcn_sched_barrier(0);
+    put(dv[kb], dv_scale, a.dv, 2 * a.H * D, kb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 }  // namespace
 
 // Waves per SIMD the head_dim-64 kernels are compiled for (register budget 512/OCC per lane):
@@ -1299,6 +1579,18 @@ static int tile_keys(int which) {
   int v[2] = {defaults[0], defaults[1]};
   sscanf(env, "%d,%d", &v[0], &v[1]);
   return v[which];
+}
+
+// Backward form (D = 64, non-causal, no ALiBi, S % 128 == 0, S <= 512): DTD_ATTN_BWD=fused selects
+// attn_bwd_fused_kernel (one workgroup per head, dQ reduced in LDS); anything else the dQ + dK/dV
+// kernel pair.
+static int g_bwd_form = -1;
+static bool bwd_fused() {
+  if (g_bwd_form < 0) {
+    const char* e = getenv("DTD_ATTN_BWD");
+    g_bwd_form = e && strcmp(e, "fused") == 0 ? 1 : 0;
+  }
+  return g_bwd_form == 1;
 }
 
 // q,k,v,o: bf16 views with row stride ld (q/k/v) / ldo (o); lse: [B,H,S] fp32.
@@ -1351,6 +1643,13 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
   DTD_LAUNCH_CHECK();
 }
 
+// 1 = fused backward where it applies, 0 = the dQ + dK/dV pair; returns the previous form
+DTD_EXPORT int dtd_attn_set_bwd_form(int f) {
+  const int old = bwd_fused() ? 1 : 0;
+  g_bwd_form = f ? 1 : 0;
+  return old;
+}
+
 // Dropout keep-bit masks of one attention call ([2][B*H*S*W] uint32), VALU-only: launched on a
 // side stream so it runs concurrently with the (MFMA-bound) QKV projection GEMM.
 DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, const uint64_t* rng, uint32_t sid,
@@ -1388,6 +1687,21 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   BwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (const bf16*)o,
             (bf16*)dq, (bf16*)dk, (bf16*)dv, slopes, mA, mB, B, S, H, ld, ldo, causal, W, scale, p,
             D == 64 ? bias_part : nullptr};
+  if (D == 64 && !causal && !slopes && S % 128 == 0 && S <= 512 && bwd_fused()) {
+    const bool drop = mA != nullptr;
+    const dim3 g1(B * H);
+    switch (S / 128) {
+      case 1: if (drop) hipLaunchKernelGGL((attn_bwd_fused_kernel<1, true>), g1, dim3(256), 0, s, a);
+              else hipLaunchKernelGGL((attn_bwd_fused_kernel<1, false>), g1, dim3(256), 0, s, a); break;
+      case 2: if (drop) hipLaunchKernelGGL((attn_bwd_fused_kernel<2, true>), g1, dim3(256), 0, s, a);
+              else hipLaunchKernelGGL((attn_bwd_fused_kernel<2, false>), g1, dim3(256), 0, s, a); break;
+      case 3: if (drop) hipLaunchKernelGGL((attn_bwd_fused_kernel<3, true>), g1, dim3(256), 0, s, a);
+              else hipLaunchKernelGGL((attn_bwd_fused_kernel<3, false>), g1, dim3(256), 0, s, a); break;
+      default: if (drop) hipLaunchKernelGGL((attn_bwd_fused_kernel<4, true>), g1, dim3(256), 0, s, a);
+               else hipLaunchKernelGGL((attn_bwd_fused_kernel<4, false>), g1, dim3(256), 0, s, a); break;
+    }
+    DTD_LAUNCH_CHECK();
+  }
   // dQ first: it also produces delta = rowsum(dO * O), which the dK/dV kernel then reads
   if (D == 64) {
     const int o = occupancy(2);

@@ -4,7 +4,8 @@ variants (DTD_ATTN_OCC="fwd,dkdv,dq" waves/SIMD).  Prints one JSON line per vari
 
 fwd_us: forward kernel with the dropout keep bits generated ahead (as in the model, where the
 mask kernel runs on a side stream under the forward GEMMs); mask_us: the mask generator alone;
-bwd_us: dK/dV + dQ.  Env: B, H, P, CAUSAL=1 (model FLOPs are quoted for the full square).  """
+bwd_us: dK/dV + dQ, or the one-kernel fused backward for a variant named "fused" (or "fused:<occ>").
+Env: B, H, P, CAUSAL=1 (model FLOPs are quoted for the full square).  """
 import json
 import os
 import sys
@@ -42,6 +43,9 @@ def main():
         A.attn_fwd(qkv, B, S, H, D, causal, None, p, rng, 3)
     torch.cuda.synchronize()
     for occ in sys.argv[1:] or ["1,1,1", "2,2,2", "3,2,2", "3,2,3"]:
+        form = "fused" if occ.startswith("fused") else "split"
+        A.set_bwd_form(form)
+        occ = occ.split(":", 1)[1] if occ.startswith("fused:") else ("3,2,3" if form == "fused" else occ)
         os.environ["DTD_ATTN_OCC"] = occ
         pend = A.attn_masks_async(B, S, H, D, p, rng, 3, qkv.device) if p > 0 else None
         torch.cuda.synchronize()
@@ -51,7 +55,7 @@ def main():
         tm = timeit(lambda: cur.wait_event(A.attn_masks_async(B, S, H, D, p, rng, 3, qkv.device).event)) \
             if p > 0 else 0.0
         tb = timeit(lambda: A.attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, causal, None, p, rng, 3, mk))
-        print(json.dumps({"occ": occ, "B": B, "S": S, "H": H, "causal": causal, "p": p, "fwd_us": round(tf, 1), "mask_us": round(tm, 1),
+        print(json.dumps({"occ": occ, "bwd_form": form, "B": B, "S": S, "H": H, "causal": causal, "p": p, "fwd_us": round(tf, 1), "mask_us": round(tm, 1),
                           "bwd_us": round(tb, 1), "fwd_TFs": round(flops_f / tf / 1e6, 1),
                           "bwd_TFs": round(2.5 * flops_f / tb / 1e6, 1)}), flush=True)
 

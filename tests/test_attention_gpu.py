@@ -67,6 +67,41 @@ def test_flash_attention_fwd_bwd(B, S, H, D, causal, alibi, p, fwd, monkeypatch)
     assert ((db - 0.25) - ref_db).abs().max().item() <= 1e-3 * (ref_db.abs().max().item() + 1.0)
 
 
+@pytest.mark.parametrize("S,p", [(512, 0.1), (512, 0.0), (384, 0.1), (256, 0.0), (128, 0.1)])
+def test_fused_backward_matches_reference_and_split(S, p):
+    """attn_bwd_fused_kernel (one workgroup per (batch, head), dQ summed in LDS, no atomics) vs the
+    fp32 math reference and vs the split dQ + dK/dV kernels; the qkv-bias column sums from its
+    epilogues equal the column sums of the dqkv it wrote.  H = 3 so (batch, head) decoding and
+    the bias rows of several heads are exercised."""
+    B, H, D = 2, 3, 64
+    torch.manual_seed(1)
+    qkv = torch.randn(B * S, 3 * H * D).to(torch.bfloat16)
+    dctx = torch.randn(B * S, H * D).to(torch.bfloat16)
+    rg, rc = RngState(5, device="cuda"), RngState(5, device="cpu")
+    assert A.fused_bwd_applies(S, D, False, None)
+    ctx_g, lse_g, mk = A.attn_fwd(qkv.cuda(), B, S, H, D, False, None, p, rg, 3)
+    ctx_r, lse_r = A.attn_fwd_ref(qkv, B, S, H, D, False, None, p, rc, 3)
+    dq_r = A.attn_bwd_ref(dctx, qkv, ctx_r, lse_r, B, S, H, D, False, None, p, rc, 3).view(B, S, 3, H, D)
+    out = {}
+    for form in ("split", "fused"):
+        prev = A.set_bwd_form(form)
+        try:
+            db = torch.zeros(3 * H * D, device="cuda", dtype=torch.float32)
+            g = A.attn_bwd(dctx.cuda(), qkv.cuda(), ctx_g, lse_g, B, S, H, D, False, None, p, rg, 3, mk,
+                           dbias=(db, True))
+            torch.cuda.synchronize()
+        finally:
+            A.set_bwd_form(prev)
+        out[form] = g
+        gv = g.view(B, S, 3, H, D).cpu()
+        for i, name in enumerate("qkv"):
+            e = rel(gv[:, :, i], dq_r[:, :, i])
+            assert e < 2e-2, f"{form} d{name} rel err {e}"
+        ref_db = g.float().sum(0)
+        assert (db - ref_db).abs().max().item() <= 1e-3 * (ref_db.abs().max().item() + 1.0), form
+    assert rel(out["fused"], out["split"]) < 1e-2
+
+
 @pytest.mark.parametrize("B,S,H,D,causal,alibi,p", [c for c in CASES if c[3] == 64] + [(4, 512, 12, 64, False, False, 0.1)])
 def test_pipelined_forward_is_bitwise_the_single_stage_forward(B, S, H, D, causal, alibi, p, monkeypatch):
     """attn_fwd_pipe_kernel (next tile's score MFMAs under this tile's softmax) reorders issue,
