@@ -1,20 +1,18 @@
 #!/usr/bin/env bash
-# Round 4 session 2b: what session 2 did not reach (it stopped at the graphed ZeRO-2 capture crash),
-# the risky graphed-ZeRO-collectives test last.
+# Round 4 session 2b: fused attention backward (numerics, kernel time, whole step), the fp32 GEMM,
+# ZeRO at world 2 on one GPU, the gemm4 probe and the force-collectives benches.
 cd "${GRAFT_REPO_ROOT}"
 source scripts/gpu_step.sh
 export TMPDIR=/tmp
-step tests_zero_w2 400 python -u -m pytest -v --timeout 180 --timeout-method thread tests/test_parallel_gpu.py -k two_ranks
-step gemm4_probe 500 python scripts/gemm4_probe.py
-step bench_force 300 python bench.py --force-collectives
+step tests_attn_fused 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_attention_gpu.py -k fused
+if grep -q " passed" gpurun_out/tests_attn_fused.log && ! grep -q "failed" gpurun_out/tests_attn_fused.log; then
+  step bench_attn 200 env B=256 python scripts/bench_attn.py 3,2,3 fused 3,2,3 fused
+  step bench_fused 300 env DTD_ATTN_BWD=fused python bench.py
+fi
 step bench_default 300 python bench.py
-step bench_b4_graph_force 300 python bench.py --batch-size 4 --graph on --force-collectives --steps 50 --warmup 10
-step bench_b4_graph 300 python bench.py --batch-size 4 --graph on --steps 50 --warmup 10
 step tests_gemm_f32 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gemm_f32_gpu.py
 step bench_f32_gemm 200 python scripts/bench_f32_gemm.py
-step bench_fp32_b32 400 python bench.py --dtype fp32 --batch-size 32 --steps 5 --warmup 2
-step bench_fp32_b32_hand 400 env DTD_GEMM_F32=1 python bench.py --dtype fp32 --batch-size 32 --steps 5 --warmup 2
-step bench_fp32_ref_b32 400 python bench.py --dtype fp32 --impl reference --batch-size 32 --steps 5 --warmup 2
-step prof_force 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_force -o run --output-format csv -- python bench.py --force-collectives --steps 3 --warmup 2
-step tests_graph_rccl 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_graph_gpu.py -k rccl
+step tests_zero_w2 400 python -u -m pytest -v --timeout 180 --timeout-method thread tests/test_parallel_gpu.py -k two_ranks
+step bench_force 300 python bench.py --force-collectives
+step gemm4_probe 400 python scripts/gemm4_probe.py
 echo done
