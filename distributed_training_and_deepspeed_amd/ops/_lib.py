@@ -77,6 +77,7 @@ _SIGS = {
     "dtd_gemm_bt_part_rows": (I, [I]),
     "dtd_gemm_bt": (I, [I, P, I, P, I, P, I, P, P, I, P, P, I, I, I, P, P]),
     "dtd_spin_occupy": (I, [I, ctypes.c_double, P]),
+    "dtd_gemm_set_stagger": (I, [ctypes.c_double]),
     "dtd_transpose_bf16": (I, [P, P, I, I, P]),
     "dtd_transpose_many": (I, [P, P, P, P, I, P]),
     "dtd_gemm_set_stamps": (I, [P]),

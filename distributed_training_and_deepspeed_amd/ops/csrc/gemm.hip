@@ -89,6 +89,7 @@ struct GemmArgs {
   int M, N, K, lda, ldb, ldc, ldu;
   unsigned long long* stamps;            // diagnostic builds only (-DDTD_GEMM_STAMPS), else null
   int* sched;                            // persistent form: dynamic tile queue (see below) or null
+  int stagger;                           // persistent form: start delay (10 ns ticks) of odd members
 };
 
 // Dynamic tile queue of the persistent form: sched[x] (x = 0..7) is the next unclaimed tile of XCD
@@ -759,6 +760,14 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
     if constexpr (DYN) sched_finish(g.sched, nwg, tid);
     return;
   }
+  // Start stagger (DTD_GEMM_STAGGER_US, experiment): the odd members of each XCD group start
+  // later, so the CUs' epilogue store bursts (128 KiB a tile) fall under other CUs' main loops
+  // instead of all CUs writing at once with their MFMA pipes idle.  Bounded wait on the real-time
+  // counter; the dynamic queue re-balances the tiles.
+  if (g.stagger > 0 && (l & 1)) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)g.stagger) __builtin_amdgcn_s_sleep(8);
+  }
   int m0, n0;
   tile_of(t, ntn, m0, n0);
   const StageOffs so = stage_offsets(w, lane, g.lda, g.ldb);
@@ -1122,6 +1131,20 @@ static int num_cus() {
   return n;
 }
 
+// persistent-form start stagger in 10 ns ticks (DTD_GEMM_STAGGER_US; dtd_gemm_set_stagger)
+static int g_stagger = -1;
+static int gemm_stagger() {
+  if (g_stagger < 0) {
+    const char* e = getenv("DTD_GEMM_STAGGER_US");
+    g_stagger = e ? (int)(atof(e) * 100.0) : 0;
+  }
+  return g_stagger;
+}
+DTD_EXPORT int dtd_gemm_set_stagger(double us) {
+  g_stagger = us > 0 ? (int)(us * 100.0) : 0;
+  return 0;
+}
+
 static unsigned long long* g_stamps = nullptr;
 // diagnostic builds: device buffer of [workgroups][32 tiles][8] u64 stamps (null: off)
 DTD_EXPORT int dtd_gemm_set_stamps(void* p) {
@@ -1150,7 +1173,7 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
   if (is_gelu_fwd(epi) && !c2) return (int)hipErrorInvalidValue;
   if (is_gelu_bwd(epi) && !u) return (int)hipErrorInvalidValue;
   GemmArgs g{(const bf16*)a, (const bf16*)b, (bf16*)c, (bf16*)c2, (const bf16*)u, (const bf16*)bias, part,
-             M, N, K, lda, ldb, ldc, ldu, g_stamps, nullptr};
+             M, N, K, lda, ldb, ldc, ldu, g_stamps, nullptr, gemm_stagger()};
   const int ntiles = (M / BM) * (N / BN);
   if (gemm_variant() >= 1) {
     const int cus = num_cus() / 8 * 8;

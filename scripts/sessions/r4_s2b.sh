@@ -10,6 +10,7 @@ if grep -q " passed" gpurun_out/tests_attn_fused.log && ! grep -q "failed" gpuru
   step bench_fused 300 env DTD_ATTN_BWD=fused python bench.py
 fi
 step bench_default 300 python bench.py
+step gemm_stagger 240 python scripts/bench_gemm_stagger.py
 step tests_gemm_f32 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gemm_f32_gpu.py
 step bench_f32_gemm 200 python scripts/bench_f32_gemm.py
 step tests_zero_w2 400 python -u -m pytest -v --timeout 180 --timeout-method thread tests/test_parallel_gpu.py -k two_ranks
