@@ -110,12 +110,16 @@ def _warn_once():
         _WARNED.append(1)
 
 
+_BWD_FORMS = ("split", "fused", "fused4")
+
+
 def set_bwd_form(form: str) -> str:
-    """'fused': one-kernel backward (attn_bwd_fused_kernel: one workgroup per (batch, head), dQ
-    reduced in LDS) where it applies -- head_dim 64, no causal mask / ALiBi, S % 128 == 0, S <= 512;
-    'split': the dQ + dK/dV kernel pair.  Returns the previous form."""
-    old = _lib.lib().dtd_attn_set_bwd_form(1 if form == "fused" else 0)
-    return "fused" if old else "split"
+    """'fused': one-kernel backward (one workgroup per (batch, head), dQ summed in LDS) where it
+    applies -- head_dim 64, no causal mask / ALiBi, S % 128 == 0, S <= 512; 8 waves (two per SIMD)
+    at S = 256 / 512, else 4.  'fused4': the 4-wave form at every S.  'split': the dQ + dK/dV
+    kernel pair.  Returns the previous form."""
+    old = _lib.lib().dtd_attn_set_bwd_form(_BWD_FORMS.index(form))
+    return _BWD_FORMS[old]
 
 
 def fused_bwd_applies(S: int, D: int, causal: bool, slopes) -> bool:

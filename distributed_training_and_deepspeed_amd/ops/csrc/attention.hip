@@ -1560,6 +1560,234 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_fused_kernel(BwdArgs a) {
   }
 }
 
+// Eight-wave form of the fused backward (S = 256 or 512): two waves per SIMD, so one wave's
+// softmax VALU runs under the other's MFMAs (the 4-wave form's single wave per SIMD serialises its
+// MFMA -> VALU -> MFMA chain: 1.6 ms against the split pair's 1.18 ms at B 256 x H 12).  Wave w
+// owns KPW = S / 8 keys (dK^T / dV^T of one or two 32-key blocks: 64 or 128 accumulator
+// registers); one key block per wave per round (dS^T image of 256 keys, 18 KiB); the dQ^T
+// 16x16x32 blocks: wave w takes head dims 16 (w & 3) .. +15 of query half w >> 2 over every key
+// of the round, so each block is a complete sum; the query-half pairs combine only their
+// qkv-bias column sums, through LDS.  The tile staging (Q, dO, O rows, lse, delta) runs on the
+// first 256 threads.
+template <int NKBW, bool DROP>
+__global__ void __launch_bounds__(512, 1) attn_bwd_fused8_kernel(BwdArgs a) {
+  constexpr int D = 64, NC = 4, NDB = 2, KPW = 32 * NKBW, SK = 8 * KPW, NT = SK / 32, NH = NKBW;
+  constexpr int DSP = 36, DSR = 8 * 32;
+  struct Smem {
+    float lse_s[32], del_s[32];
+    float csq[64];           // query-half-1 dQ column sums, per head dim
+    bf16 Qs[32 * 64];
+    bf16 Os[32 * 64];
+    bf16 DS[DSR * DSP];
+    bf16 Ks[SK * 64];
+    bf16 Vs[SK * 64];
+  };
+  __shared__ __attribute__((aligned(16))) Smem sm;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5,
+            r = lane & 31;
+  const bool stager = tid < 256;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int S = a.S;   // == SK (host-checked)
+  const float sc2 = a.scale * kLog2e;
+  const float inv_keep = DROP ? 1.f / (1.f - a.p) : 1.f;
+  const int kw0 = w * KPW;
+  const int Sp = 32 * a.W;
+  const float* lseb = a.lse + (size_t)bh * S;
+  const RowSrc qsrc = row_src<D>(a.q + (size_t)b * S * a.ld + h * D, a.ld, S);
+  const RowSrc dsrc = row_src<D>(a.dout + (size_t)b * S * a.ldo + h * D, a.ldo, S);
+  const RowSrc osrc = row_src<D>(a.o + (size_t)b * S * a.ldo + h * D, a.ldo, S);
+  if (stager) {
+    const RowSrc ksrc = row_src<D>(a.k + (size_t)b * S * a.ld + h * D, a.ld, S);
+    const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
+#pragma unroll
+    for (int part = 0; part < SK / 128; ++part) {
+      TileLoader<D, 128> kl, vl;
+      kl.load(ksrc, part * 128);
+      vl.load(vsrc, part * 128);
+      kl.store_swz(sm.Ks + part * 128 * 64);
+      vl.store_swz(sm.Vs + part * 128 * 64);
+    }
+  }
+  TileLoader<D, 32> ql, dl, ol;
+  float lse_n = 0.f;
+  auto fetch = [&](int q0) {
+    if (!stager) return;
+    ql.load(qsrc, q0);
+    dl.load(dsrc, q0);
+    ol.load(osrc, q0);
+    if (tid < 32) lse_n = lseb[q0 + tid];
+  };
+  auto stage = [&]() {
+    if (!stager) return;
+    float part = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part = fmaf((float)dl.reg[0][j], (float)ol.reg[0][j], part);
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    part += __shfl_xor(part, 4, 64);
+    ql.store_swz(sm.Qs);
+    dl.store_swz(sm.Os);
+    if ((tid & 7) == 0) sm.del_s[tid >> 3] = -part;
+    if (tid < 32) sm.lse_s[tid] = -lse_n * kLog2e;
+  };
+  fetch(0);
+  stage();
+
+  f32x16 dk[NKBW][NDB], dv[NKBW][NDB];
+#pragma unroll
+  for (int kb = 0; kb < NKBW; ++kb)
+#pragma unroll
+    for (int d = 0; d < NDB; ++d) { dk[kb][d] = f32x16{}; dv[kb][d] = f32x16{}; }
+  const int g16 = lane >> 4, l16 = lane & 15, qq = l16 >> 2, pp = l16 & 3;
+  const int dd = w & 3, qh = w >> 2;
+  const int kcol = 16 * dd + 4 * pp;
+  __syncthreads();
+
+  for (int t = 0; t < NT; ++t) {
+    const int q0 = t * 32;
+    if (t + 1 < NT) fetch(q0 + 32);
+    f32x4 dq1 = f32x4{};
+#pragma unroll
+    for (int kb = 0; kb < NH; ++kb) {
+      const int key0 = kw0 + 32 * kb;
+      f32x16 sacc = f32x16{}, pacc = f32x16{};
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        sacc = mfma32(swz_row_read(sm.Qs, 0, r, 2 * c + hh), swz_row_read(sm.Ks, key0, r, 2 * c + hh), sacc);
+        pacc = mfma32(swz_row_read(sm.Os, 0, r, 2 * c + hh), swz_row_read(sm.Vs, key0, r, 2 * c + hh), pacc);
+      }
+      // fragments read just ahead of their MFMAs (4 reads, 2 MFMAs per group): hoisting all 16
+      // reads made this block the register peak (dK/dV accumulators + 64 fragment registers)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
+      uint64_t mk[16];
+      if constexpr (DROP) {
+        const cu64* mp = (const cu64*)(uintptr_t)(a.maskA + ((size_t)bh * a.W + (w * NKBW + kb)) * Sp + q0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mk[i] = mp[i];
+      }
+      f32x4 L4[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) L4[g] = *reinterpret_cast<const f32x4*>(&sm.lse_s[8 * g + 4 * hh]);
+      const f32x2 sc2v = pk2(sc2, sc2);
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const f32x2 x = pk_fma(pk2(sacc[i], sacc[i + 1]), sc2v, pk2(L4[i >> 2][i & 3], L4[i >> 2][(i & 3) + 1]));
+        sacc[i] = fexp2(x.x);
+        sacc[i + 1] = fexp2(x.y);
+      }
+      f32x4 D4[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) D4[g] = *reinterpret_cast<const f32x4*>(&sm.del_s[8 * g + 4 * hh]);
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const f32x2 nd = pk2(D4[i >> 2][i & 3], D4[i >> 2][(i & 3) + 1]);
+        if constexpr (DROP) {
+          const f32x2 tt = pk_fma(pk2(sel_keep(pacc[i], mk[i]), sel_keep(pacc[i + 1], mk[i + 1])),
+                                  pk2(inv_keep, inv_keep), nd);
+          const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * tt;
+          pacc[i] = ds.x;
+          pacc[i + 1] = ds.y;
+          sacc[i] = sel_keep(sacc[i], mk[i]);
+          sacc[i + 1] = sel_keep(sacc[i + 1], mk[i + 1]);
+        } else {
+          const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * (pk2(pacc[i], pacc[i + 1]) + nd);
+          pacc[i] = ds.x;
+          pacc[i + 1] = ds.y;
+        }
+      }
+      bf16* dsrow = sm.DS + (w * 32 + r) * DSP + 4 * hh;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pb, sb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { pb[j] = (bf16)sacc[8 * s2 + j]; sb[j] = (bf16)pacc[8 * s2 + j]; }
+#pragma unroll
+        for (int d = 0; d < NDB; ++d) {
+          dv[kb][d] = mfma32(tr_operand_swz(sm.Os, 16 * s2, d * 32, lane), pb, dv[kb][d]);
+          dk[kb][d] = mfma32(tr_operand_swz(sm.Qs, 16 * s2, d * 32, lane), sb, dk[kb][d]);
+        }
+        *reinterpret_cast<bf16x4*>(dsrow + 16 * s2) = __builtin_shufflevector(sb, sb, 0, 1, 2, 3);
+        *reinterpret_cast<bf16x4*>(dsrow + 16 * s2 + 8) = __builtin_shufflevector(sb, sb, 4, 5, 6, 7);
+      }
+      __syncthreads();   // the round's dS^T image complete
+      // dQ^T rows 16 dd .. +15 x queries 16 qh .. +15 over the round's 256 keys (32 of each wave)
+#pragma unroll 1
+      for (int k0 = 0; k0 < DSR; k0 += 32) {
+        const int key = (k0 / 32) * KPW + kb * 32 + 8 * g16 + qq;
+        const bf16* ka = sm.Ks + key * 64 + 8 * ((kcol >> 3) ^ swz64(key)) + (kcol & 7);
+        const bf16* kb4 = sm.Ks + (key + 4) * 64 + 8 * ((kcol >> 3) ^ swz64(key + 4)) + (kcol & 7);
+        const int lr = k0 + 8 * g16 + qq;
+        const bf16* dp = sm.DS + lr * DSP + 16 * qh + 4 * pp;
+        dq1 = mfma16(cat(tr_read(ka), tr_read(kb4)), cat(tr_read(dp), tr_read(dp + 4 * DSP)), dq1);
+      }
+      float cs[4] = {0.f, 0.f, 0.f, 0.f};
+      if (kb == NH - 1) {
+        // lane: query q0 + 16 qh + l16, head dims 16 dd + 4 g16 + 0..3 -- a complete sum
+        bf16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v4[j] = (bf16)(dq1[j] * a.scale);
+          cs[j] = (float)v4[j];
+        }
+        *reinterpret_cast<bf16x4*>(a.dq + (size_t)(b * S + q0 + 16 * qh + l16) * a.ld + h * D + 16 * dd + 4 * g16) = v4;
+        if (a.bias_part) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            cs[j] += __shfl_xor(cs[j], 1, 64);
+            cs[j] += __shfl_xor(cs[j], 2, 64);
+            cs[j] += __shfl_xor(cs[j], 4, 64);
+            cs[j] += __shfl_xor(cs[j], 8, 64);
+          }
+          if (qh == 1 && l16 == 0)
+            *reinterpret_cast<f32x4*>(&sm.csq[16 * dd + 4 * g16]) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+        }
+        if (t + 1 < NT) stage();
+      }
+      __syncthreads();   // the image consumed (after the last round: the next tile staged, the
+                         // query-half-1 column sums published)
+      if (kb == NH - 1 && a.bias_part && qh == 0 && l16 == 0) {
+        const f32x4 o4 = *reinterpret_cast<const f32x4*>(&sm.csq[16 * dd + 4 * g16]);
+        *reinterpret_cast<f32x4*>(a.bias_part + ((size_t)b * (S / 32) + t) * (3 * a.H * D) + h * D + 16 * dd + 4 * g16) =
+            f32x4{cs[0] + o4[0], cs[1] + o4[1], cs[2] + o4[2], cs[3] + o4[3]};
+      }
+    }
+  }
+  const float dv_scale = inv_keep;
+  auto put = [&](const f32x16 (&acc)[NDB], float sc, bf16* dst, int colbase, int kb) {
+    if (a.bias_part) {
+      float vk[32];
+#pragma unroll
+      for (int d = 0; d < NDB; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) vk[16 * d + i] = (float)(bf16)(acc[d][i] * sc);
+      const float sk = colsum32(vk, r);
+      a.bias_part[((size_t)b * (S / 32) + w * NKBW + kb) * (3 * a.H * D) + colbase + h * D + colsum_col(r, hh)] = sk;
+    }
+    bf16* p = dst + (size_t)(b * S + kw0 + 32 * kb + r) * a.ld + h * D;
+#pragma unroll
+    for (int d = 0; d < NDB; ++d)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        bf16x4 k4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k4[j] = (bf16)(acc[d][4 * gq + j] * sc);
+        *reinterpret_cast<bf16x4*>(p + d * 32 + 8 * gq + 4 * hh) = k4;
+      }
+  };
+#pragma unroll
+  for (int kb = 0; kb < NKBW; ++kb) {
+    put(dk[kb], a.scale, a.dk, a.H * D, kb);
+    __builtin_amdgcn_sched_barrier(0);
+    put(dv[kb], dv_scale, a.dv, 2 * a.H * D, kb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 }  // namespace
 
 // Waves per SIMD the head_dim-64 kernels are compiled for (register budget 512/OCC per lane):
@@ -1608,14 +1836,18 @@ static int tile_keys(int which) {
 // Backward form (D = 64, non-causal, no ALiBi, S % 128 == 0, S <= 512): DTD_ATTN_BWD=fused selects
 // attn_bwd_fused_kernel (one workgroup per head, dQ reduced in LDS); anything else the dQ + dK/dV
 // kernel pair.
+// form: 0 = split pair, 1 = fused (8 waves at S = 256 / 512, else 4), 2 = fused, 4 waves always.
+// DTD_ATTN_BWD=fused / fused4 / split; dtd_attn_set_bwd_form at run time.
 static int g_bwd_form = -1;
-static bool bwd_fused() {
+static int bwd_form() {
   if (g_bwd_form < 0) {
     const char* e = getenv("DTD_ATTN_BWD");
-    g_bwd_form = e && strcmp(e, "fused") == 0 ? 1 : 0;
+    g_bwd_form = !e ? 0 : strcmp(e, "fused") == 0 ? 1 : strcmp(e, "fused4") == 0 ? 2 : 0;
   }
-  return g_bwd_form == 1;
+  return g_bwd_form;
 }
+static bool bwd_fused() { return bwd_form() != 0; }
+static bool bwd_fused8() { return bwd_form() == 1; }
 
 // q,k,v,o: bf16 views with row stride ld (q/k/v) / ldo (o); lse: [B,H,S] fp32.
 // masks: [2][B*H*S*W] uint32 (W = ceil(S/32)) written here when p > 0 (read by the backward).
@@ -1667,10 +1899,10 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
   DTD_LAUNCH_CHECK();
 }
 
-// 1 = fused backward where it applies, 0 = the dQ + dK/dV pair; returns the previous form
+// 0 = the dQ + dK/dV pair, 1 = fused where it applies, 2 = fused, 4-wave form; returns the previous
 DTD_EXPORT int dtd_attn_set_bwd_form(int f) {
-  const int old = bwd_fused() ? 1 : 0;
-  g_bwd_form = f ? 1 : 0;
+  const int old = bwd_form();
+  g_bwd_form = f < 0 || f > 2 ? 0 : f;
   return old;
 }
 
@@ -1714,6 +1946,16 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   if (D == 64 && !causal && !slopes && S % 128 == 0 && S <= 512 && bwd_fused()) {
     const bool drop = mA != nullptr;
     const dim3 g1(B * H);
+    if ((S == 256 || S == 512) && bwd_fused8()) {
+      if (S == 512) {
+        if (drop) hipLaunchKernelGGL((attn_bwd_fused8_kernel<2, true>), g1, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((attn_bwd_fused8_kernel<2, false>), g1, dim3(512), 0, s, a);
+      } else {
+        if (drop) hipLaunchKernelGGL((attn_bwd_fused8_kernel<1, true>), g1, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((attn_bwd_fused8_kernel<1, false>), g1, dim3(512), 0, s, a);
+      }
+      DTD_LAUNCH_CHECK();
+    }
     switch (S / 128) {
       case 1: if (drop) hipLaunchKernelGGL((attn_bwd_fused_kernel<1, true>), g1, dim3(256), 0, s, a);
               else hipLaunchKernelGGL((attn_bwd_fused_kernel<1, false>), g1, dim3(256), 0, s, a); break;

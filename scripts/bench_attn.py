@@ -43,9 +43,9 @@ def main():
         A.attn_fwd(qkv, B, S, H, D, causal, None, p, rng, 3)
     torch.cuda.synchronize()
     for occ in sys.argv[1:] or ["1,1,1", "2,2,2", "3,2,2", "3,2,3"]:
-        form = "fused" if occ.startswith("fused") else "split"
+        form = occ.split(":", 1)[0] if occ.startswith("fused") else "split"
         A.set_bwd_form(form)
-        occ = occ.split(":", 1)[1] if occ.startswith("fused:") else ("3,2,3" if form == "fused" else occ)
+        occ = occ.split(":", 1)[1] if ":" in occ else ("3,2,3" if form != "split" else occ)
         os.environ["DTD_ATTN_OCC"] = occ
         pend = A.attn_masks_async(B, S, H, D, p, rng, 3, qkv.device) if p > 0 else None
         torch.cuda.synchronize()

@@ -22,12 +22,13 @@ def main():
         rg = RngState(5, device="cuda")
         ctx, lse, mk = A.attn_fwd(qkv, B, S, H, D, False, None, p, rg, 3)
         out = {}
-        for form in ("split", "fused", "fused2"):
-            A.set_bwd_form("split" if form == "split" else "fused")
+        for form in ("split", "fused", "fused2", "fused4"):
+            A.set_bwd_form({"split": "split", "fused4": "fused4"}.get(form, "fused"))
             out[form] = A.attn_bwd(dctx, qkv, ctx, lse, B, S, H, D, False, None, p, rg, 3, mk).float()
             torch.cuda.synchronize()
         A.set_bwd_form("split")
-        rep = {"S": S, "p": p, "fused_repeatable": bool(torch.equal(out["fused"], out["fused2"]))}
+        rep = {"S": S, "p": p, "fused_repeatable": bool(torch.equal(out["fused"], out["fused2"])),
+               "fused4_vs_split": float((out["fused4"] - out["split"]).abs().max())}
         g = out["fused"].view(B, S // 32, 32, 3, H, D)
         r = out["split"].view(B, S // 32, 32, 3, H, D)
         for i, name in enumerate("qkv"):

@@ -83,7 +83,7 @@ def test_fused_backward_matches_reference_and_split(S, p):
     ctx_r, lse_r = A.attn_fwd_ref(qkv, B, S, H, D, False, None, p, rc, 3)
     dq_r = A.attn_bwd_ref(dctx, qkv, ctx_r, lse_r, B, S, H, D, False, None, p, rc, 3).view(B, S, 3, H, D)
     out = {}
-    for form in ("split", "fused"):
+    for form in ("split", "fused", "fused4"):
         prev = A.set_bwd_form(form)
         try:
             db = torch.zeros(3 * H * D, device="cuda", dtype=torch.float32)
@@ -100,6 +100,7 @@ def test_fused_backward_matches_reference_and_split(S, p):
         ref_db = g.float().sum(0)
         assert (db - ref_db).abs().max().item() <= 1e-3 * (ref_db.abs().max().item() + 1.0), form
     assert rel(out["fused"], out["split"]) < 1e-2
+    assert rel(out["fused4"], out["split"]) < 1e-2
 
 
 @pytest.mark.parametrize("B,S,H,D,causal,alibi,p", [c for c in CASES if c[3] == 64] + [(4, 512, 12, 64, False, False, 0.1)])
