@@ -116,7 +116,7 @@ _BWD_FORMS = ("split", "fused", "fused4")
 def set_bwd_form(form: str) -> str:
     """'fused': one-kernel backward (one workgroup per (batch, head), dQ summed in LDS) where it
     applies -- head_dim 64, no causal mask / ALiBi, S % 128 == 0, S <= 512; 8 waves (two per SIMD)
-    at S = 256 / 512, else 4.  'fused4': the 4-wave form at every S.  'split': the dQ + dK/dV
+    at S = 512, else 4.  'fused4': the 4-wave form at every S.  'split': the dQ + dK/dV
     kernel pair.  Returns the previous form."""
     old = _lib.lib().dtd_attn_set_bwd_form(_BWD_FORMS.index(form))
     return _BWD_FORMS[old]

@@ -1836,7 +1836,9 @@ static int tile_keys(int which) {
 // Backward form (D = 64, non-causal, no ALiBi, S % 128 == 0, S <= 512): DTD_ATTN_BWD=fused selects
 // attn_bwd_fused_kernel (one workgroup per head, dQ reduced in LDS); anything else the dQ + dK/dV
 // kernel pair.
-// form: 0 = split pair, 1 = fused (8 waves at S = 256 / 512, else 4), 2 = fused, 4 waves always.
+// form: 0 = split pair, 1 = fused (8 waves at S = 512, else 4), 2 = fused, 4 waves always.
+// Measured at B 256 x H 12 x S 512 (scripts/bench_attn.py): split 1.16-1.17 ms, fused 8-wave
+// 1.18 ms, fused 4-wave 1.60 ms -- the split pair stays the default.
 // DTD_ATTN_BWD=fused / fused4 / split; dtd_attn_set_bwd_form at run time.
 static int g_bwd_form = -1;
 static int bwd_form() {
@@ -1946,14 +1948,11 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   if (D == 64 && !causal && !slopes && S % 128 == 0 && S <= 512 && bwd_fused()) {
     const bool drop = mA != nullptr;
     const dim3 g1(B * H);
-    if ((S == 256 || S == 512) && bwd_fused8()) {
-      if (S == 512) {
-        if (drop) hipLaunchKernelGGL((attn_bwd_fused8_kernel<2, true>), g1, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((attn_bwd_fused8_kernel<2, false>), g1, dim3(512), 0, s, a);
-      } else {
-        if (drop) hipLaunchKernelGGL((attn_bwd_fused8_kernel<1, true>), g1, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((attn_bwd_fused8_kernel<1, false>), g1, dim3(512), 0, s, a);
-      }
+    // (the one-key-block-per-wave instantiation, S = 256, gave wrong, run-to-run varying dS rows
+    // with dropout on the box -- unresolved, so it is not launched: S = 256 takes the 4-wave form)
+    if (S == 512 && bwd_fused8()) {
+      if (drop) hipLaunchKernelGGL((attn_bwd_fused8_kernel<2, true>), g1, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((attn_bwd_fused8_kernel<2, false>), g1, dim3(512), 0, s, a);
       DTD_LAUNCH_CHECK();
     }
     switch (S / 128) {

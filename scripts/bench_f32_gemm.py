@@ -6,8 +6,11 @@ reaches 122 TF/s at 4096^3)."""
 import json
 import os
 import statistics
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def timed(fn, reps=5):
