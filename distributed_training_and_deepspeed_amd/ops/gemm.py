@@ -105,13 +105,21 @@ def set_all(on: bool) -> None:
     _ALL[0] = bool(on)
 
 
-# fp32 (reference-precision) products on the hand-written f32-MFMA kernel (ops/csrc/gemm_f32.hip):
-# forward, NT input gradient and split-K weight gradient (DTD_GEMM_F32=1; default off until measured).
-_F32 = [os.environ.get("DTD_GEMM_F32", "0") == "1"]
+# fp32 (reference-precision) products on the hand-written f32-MFMA kernel (ops/csrc/gemm_f32.hip).
+# DTD_GEMM_F32 = "wgrad" (default): the split-K weight gradients only -- 1.36-1.52x the library's
+# fp32 wgrad at b32 x 512 tokens, while the library's forward / input-gradient GEMMs run at
+# 123-149 TF/s against the hand kernel's 110-123 (profiles/r4_s2c_results.jsonl); "1"/"all": every
+# fp32 product; "0": none.
+_F32_MODE = os.environ.get("DTD_GEMM_F32", "wgrad")
+_F32 = [_F32_MODE in ("1", "all")]
+_F32_WGRAD = [_F32_MODE in ("1", "all", "wgrad")]
 
 
-def set_f32(on: bool) -> None:
+def set_f32(on: bool, wgrad: bool | None = None) -> None:
+    """All fp32 products on the hand kernel (on) or none; ``wgrad`` sets the weight gradients
+    separately (default: follow ``on``)."""
     _F32[0] = bool(on)
+    _F32_WGRAD[0] = bool(on) if wgrad is None else bool(wgrad)
 
 
 def _ok32(t: torch.Tensor) -> bool:
@@ -119,8 +127,8 @@ def _ok32(t: torch.Tensor) -> bool:
             and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0)
 
 
-def f32_supported(M: int, N: int, K: int, *tensors) -> bool:
-    if not (_F32[0] and all(_ok32(t) for t in tensors) and _lib.has("dtd_gemm_f32_nt")):
+def f32_supported(M: int, N: int, K: int, *tensors, wgrad: bool = False) -> bool:
+    if not ((_F32_WGRAD[0] if wgrad else _F32[0]) and all(_ok32(t) for t in tensors) and _lib.has("dtd_gemm_f32_nt")):
         return False
     return bool(_lib.lib().dtd_gemm_f32_supported(M, N, K))
 

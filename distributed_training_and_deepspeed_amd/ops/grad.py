@@ -195,7 +195,7 @@ def _emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
     i = x.shape[1]
     if dy.is_cuda and dy.dtype == torch.float32:
         from . import gemm as G
-        if G.f32_supported(o, i, T, dy, x):
+        if G.f32_supported(o, i, T, dy, x, wgrad=True):
             # reference-precision path: the f32-MFMA TN kernel, fp32 split-K partials
             splitk_reduce(G.gemm_f32_tn(dy, x), dst, acc)
             return

@@ -19,7 +19,7 @@ def rel(a, b):
 def f32_on():
     G.set_f32(True)
     yield
-    G.set_f32(False)
+    G.set_f32(False, wgrad=True)          # back to the default: weight gradients only
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 16), (256, 384, 64), (512, 768, 768), (1024, 3072, 768),
@@ -75,7 +75,7 @@ def test_fp32_model_path_matches_library(f32_on):
     from distributed_training_and_deepspeed_amd.models import build_model
     out = []
     for on in (False, True):
-        G.set_f32(on)
+        G.set_f32(on)                     # off: library everywhere; on: every fp32 product hand-written
         model = build_model("bert-tiny", impl="fused", dtype=torch.float32, device="cuda", seed=5)
         ds = SyntheticLMDataset(model.cfg, 4, seq_len=128, seed=3)
         loss = model(ds.input_ids.cuda(), labels=ds.labels.cuda()).loss
