@@ -79,8 +79,10 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
         return out.loss.detach()
 
     graphed, batches, warm, loss = None, iter(loader), [], None
-    if opts.graph == "auto":  # multi-rank RCCL capture stays opt-in
-        opts.graph = "on" if (cuda and world_size == 1 and batch_size <= 32 and not opts.markers) else "off"
+    if opts.graph == "auto":
+        # small per-GPU batches are host-launch bound: replay the whole step -- bucket all-reduces
+        # included (RCCL collectives inside the capture: tests/test_graph_gpu.py, force_collectives)
+        opts.graph = "on" if (cuda and batch_size <= 32 and not opts.markers) else "off"
     if opts.graph == "on" and cuda:
         # whole step (forward, backward + bucket all-reduces, optimizer, RNG advance) replayed as
         # one hipGraph: the reference's 4 x 512-token batches are host-launch bound otherwise
@@ -149,8 +151,8 @@ if __name__ == "__main__":
     parser.add_argument("--opt-overlap", action="store_true",
                         help="stage the Adam update under the next forward (FusedAdam.overlap_with_forward)")
     parser.add_argument("--graph", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
-                        help="capture the whole training step in a hipGraph and replay it (auto: on for one GPU "
-                             "at <= 32 sequences per step, where the step is host-launch bound)")
+                        help="capture the whole training step (bucket all-reduces included) in a hipGraph and "
+                             "replay it (auto: on at <= 32 sequences per GPU, where the step is host-launch bound)")
     args = parser.parse_args()
 
     device_count = args.device_count or get_device_count()
