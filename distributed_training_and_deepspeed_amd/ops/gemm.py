@@ -106,11 +106,12 @@ def set_all(on: bool) -> None:
 
 
 # fp32 (reference-precision) products on the hand-written f32-MFMA kernel (ops/csrc/gemm_f32.hip).
-# DTD_GEMM_F32 = "wgrad" (default): the split-K weight gradients only -- 1.36-1.52x the library's
-# fp32 wgrad at b32 x 512 tokens, while the library's forward / input-gradient GEMMs run at
-# 123-149 TF/s against the hand kernel's 110-123 (profiles/r4_s2c_results.jsonl); "1"/"all": every
-# fp32 product; "0": none.
-_F32_MODE = os.environ.get("DTD_GEMM_F32", "wgrad")
+# DTD_GEMM_F32 = "wgrad": the split-K weight gradients only; "1"/"all": every fp32 product; "0"
+# (default): none.  Measured (profiles/r4_s2c_results.jsonl, r4_fp32_b32_kernel_summary.txt): the
+# library's forward / input-gradient GEMMs run at 123-149 TF/s against the hand kernel's 110-123;
+# the hand TN kernel beats a single-call library wgrad (87-98 vs 64 TF/s) but in the step it runs at
+# ~96 TF/s, slower than the library's K-sliced bmm path the step uses -- so all stay opt-in.
+_F32_MODE = os.environ.get("DTD_GEMM_F32", "0")
 _F32 = [_F32_MODE in ("1", "all")]
 _F32_WGRAD = [_F32_MODE in ("1", "all", "wgrad")]
 
