@@ -899,7 +899,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
     if (threadIdx.x < BM) {
       const int qq = q0 + threadIdx.x;
       lse_r = qq < S ? -lseb[qq] * kLog2e : 0.f;   // stored negated: P = 2^fma(s, sc2, -lse)
-      del_r = qq < S ? -delb[qq] : 0.f;            //                 dS = P (dP - delta)
+      // dS = P (dP - delta); with dropout the kernel forms dS' = (1 - p) dS = Pm dP - P (1 - p) delta
+      // (Pm = P * keep), so delta is stored pre-scaled and dK takes the 1 / (1 - p) at the end
+      del_r = qq < S ? -delb[qq] * (DROP ? 1.f - a.p : 1.f) : 0.f;
     }
   };
   // L2 prefetch of the next query tile's keep words (BM words, value unused)
@@ -986,13 +988,14 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       for (int i = 0; i < 16; i += 2) {
         const f32x2 nd = pk2(D4[i >> 2][i & 3], D4[i >> 2][(i & 3) + 1]);
         if constexpr (DROP) {
-          const f32x2 t = pk_fma(pk2(sel_keep(pacc[i], mk[i]), sel_keep(pacc[i + 1], mk[i + 1])),
-                                 pk2(inv_keep, inv_keep), nd);
-          const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * t;                 // dS
+          // 2 VALU issues per score instead of 3: one keep select (Pm feeds both dV and dS')
+          const f32x2 pm = pk2(sel_keep(sacc[i], mk[i]), sel_keep(sacc[i + 1], mk[i + 1]));
+          const f32x2 u = pk2(sacc[i], sacc[i + 1]) * nd;                 // -P (1 - p) delta
+          const f32x2 ds = pk_fma(pm, pk2(pacc[i], pacc[i + 1]), u);      // dS' = (1 - p) dS
           pacc[i] = ds.x;
           pacc[i + 1] = ds.y;
-          sacc[i] = sel_keep(sacc[i], mk[i]);                             // P*mask (dV)
-          sacc[i + 1] = sel_keep(sacc[i + 1], mk[i + 1]);
+          sacc[i] = pm.x;                                                 // P*mask (dV)
+          sacc[i + 1] = pm.y;
         } else {
           const f32x2 ds = pk2(sacc[i], sacc[i + 1]) * (pk2(pacc[i], pacc[i + 1]) + nd);
           pacc[i] = ds.x;
@@ -1024,13 +1027,14 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
     __syncthreads();
   }
   const float dv_scale = inv_keep;   // the dropped P fed to dV carried keep bits only
+  const float dk_scale = a.scale * inv_keep;   // dS' = (1 - p) dS (see load_stats)
   if (a.bias_part && D == 64) {
     float vk[32], vv[32];
 #pragma unroll
     for (int d = 0; d < NDB; ++d)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {   // the stored (bf16-rounded) values, 0 past S
-        vk[16 * d + i] = kvalid ? (float)(bf16)(dk[d][i] * a.scale) : 0.f;
+        vk[16 * d + i] = kvalid ? (float)(bf16)(dk[d][i] * dk_scale) : 0.f;
         vv[16 * d + i] = kvalid ? (float)(bf16)(dv[d][i] * dv_scale) : 0.f;
       }
     const float sk = colsum32(vk, r), sv = colsum32(vv, r);
@@ -1047,7 +1051,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
     for (int gq = 0; gq < 4; ++gq) {
       bf16x4 k4, v4;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) { k4[t] = (bf16)(dk[d][4 * gq + t] * a.scale); v4[t] = (bf16)(dv[d][4 * gq + t] * dv_scale); }
+      for (int t = 0; t < 4; ++t) { k4[t] = (bf16)(dk[d][4 * gq + t] * dk_scale); v4[t] = (bf16)(dv[d][4 * gq + t] * dv_scale); }
       *reinterpret_cast<bf16x4*>(dkp + d * 32 + 8 * gq + 4 * hh) = k4;
       *reinterpret_cast<bf16x4*>(dvp + d * 32 + 8 * gq + 4 * hh) = v4;
     }
