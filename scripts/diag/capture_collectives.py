@@ -1,0 +1,69 @@
+#!/usr/bin/env python
+"""Which RCCL collective breaks hipGraph capture at world 1?  Each case runs in its own child
+process (a crash in hipStreamEndCapture kills only that child): capture the collective on a side
+stream joined to the capturing stream, replay, compare.  Prints one JSON line per case."""
+import json
+import os
+import subprocess
+import sys
+
+CASES = ["all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor", "all_gather_coalesced", "reduce_scatter_coalesced"]
+
+
+def child(case):
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    x = torch.randn(1 << 20, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty_like(x)
+    xs = [torch.randn(1 << 18, device="cuda", dtype=torch.bfloat16) for _ in range(3)]
+    outs = [torch.empty_like(t) for t in xs]
+
+    def run():
+        if case == "all_reduce":
+            dist.all_reduce(x, op=dist.ReduceOp.AVG)
+        elif case == "reduce_scatter_tensor":
+            dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG)
+        elif case == "all_gather_into_tensor":
+            dist.all_gather_into_tensor(out, x)
+        elif case == "all_gather_coalesced":
+            with dist._coalescing_manager(async_ops=True) as cm:
+                for o, i in zip(outs, xs):
+                    dist.all_gather_into_tensor(o, i, async_op=True)
+            cm.wait()
+        elif case == "reduce_scatter_coalesced":
+            with dist._coalescing_manager(async_ops=True) as cm:
+                for o, i in zip(outs, xs):
+                    dist.reduce_scatter_tensor(o, i, op=dist.ReduceOp.AVG, async_op=True)
+            cm.wait()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run()                                   # eager warm-up (communicator, buffers)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run()
+    g.replay()
+    torch.cuda.synchronize()
+    print(json.dumps({"case": case, "captured_and_replayed": True}), flush=True)
+    dist.destroy_process_group()
+
+
+def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--child":
+        child(sys.argv[2])
+        return
+    for i, case in enumerate(CASES):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29600 + i))
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", case], env=env,
+                           capture_output=True, text=True, timeout=120)
+        ok = r.returncode == 0 and "captured_and_replayed" in r.stdout
+        print(json.dumps({"case": case, "ok": ok, "returncode": r.returncode,
+                          "err": "" if ok else r.stderr.strip().splitlines()[-1][:200] if r.stderr.strip() else ""}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
