@@ -107,7 +107,9 @@ class CommsLogger:
     def run(self, op: str, fn, tensor: torch.Tensor | None, nbytes: int, group, async_op: bool):
         """Execute collective ``fn(async_op=...)`` with timing; returns its work/None."""
         world = dist.get_world_size(group) if dist.is_initialized() else 1
-        if not self.should_log(op):
+        if not self.should_log(op) or (tensor is not None and tensor.is_cuda and torch.cuda.is_current_stream_capturing()):
+            # (inside a hipGraph capture the timing side stream would be left un-joined and the
+            # synchronising form is illegal: captured collectives are not logged)
             return fn(async_op)
         gpu = tensor is not None and tensor.is_cuda
         if gpu and not self.sync_timing:
