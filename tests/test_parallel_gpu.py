@@ -22,11 +22,12 @@ def rccl_world1():
     comm.destroy()
 
 
-def _zero_run(stage, steps=4, replicated=True):
+def _zero_run(stage, steps=4, replicated=True, force=False):
     from distributed_training_and_deepspeed_amd.parallel.zero import initialize
     model = build_model("causal-tiny", dtype=torch.bfloat16, device="cuda", seed=3)
     cfg = {"optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "comms_logger": {"enabled": True},
-           "zero_optimization": {"stage": stage, "reduce_bucket_size": 100000, "world1_replicated": replicated}}
+           "zero_optimization": {"stage": stage, "reduce_bucket_size": 100000, "world1_replicated": replicated,
+                                 "force_collectives": force}}
     eng, opt, _, _ = initialize(model=model, model_parameters=model.parameters(), config=cfg)
     ds = SyntheticLMDataset(model.cfg, 4 * steps, seq_len=128, mlm=False, seed=1)
     ids, lab = ds.input_ids.view(steps, 4, 128).cuda(), ds.labels.view(steps, 4, 128).cuda()
@@ -52,6 +53,18 @@ def test_zero_stages_on_gpu_match_stage0(rccl_world1, stage, replicated):
     assert abs(l0[-1] - ls[-1]) < 5e-3, (l0, ls)
     # world 1: every layout holds the same parameter set (different order for stage 3 units)
     assert abs(m0.sum().item() - ms.sum().item()) < 1e-2 * m0.abs().sum().item() / m0.numel() * 100 + 1e-3
+
+
+@pytest.mark.parametrize("stage", [1, 2, 3])
+def test_zero_rccl_collectives_at_world1_match_local_path(rccl_world1, stage):
+    """force_collectives: the partitioned engine issues its real RCCL reduce-scatters and refresh /
+    stage-3 all-gathers (on its comm stream, overlapped with backward) at world 1 -- and trains
+    exactly like the same engine's local stand-ins for them."""
+    ll, ml, el = _zero_run(stage, replicated=False)
+    lf, mf, ef = _zero_run(stage, replicated=False, force=True)
+    assert ef.collect and not el.collect
+    assert ll == lf, (ll, lf)
+    assert torch.equal(ml, mf)
 
 
 def test_gpipe_two_stages_one_gpu_recompute_is_exact():
