@@ -7,7 +7,8 @@ import os
 import subprocess
 import sys
 
-CASES = ["all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor", "all_gather_coalesced", "reduce_scatter_coalesced"]
+CASES = ["all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor", "all_gather_coalesced", "reduce_scatter_coalesced",
+         "all_gather_inplace", "reduce_scatter_inplace", "all_reduce_async_wait", "reduce_scatter_async_wait"]
 
 
 def child(case):
@@ -32,6 +33,14 @@ def child(case):
                 for o, i in zip(outs, xs):
                     dist.all_gather_into_tensor(o, i, async_op=True)
             cm.wait()
+        elif case == "all_gather_inplace":          # world 1: the shard IS the output
+            dist.all_gather_into_tensor(x, x)
+        elif case == "reduce_scatter_inplace":
+            dist.reduce_scatter_tensor(x, x, op=dist.ReduceOp.AVG)
+        elif case == "all_reduce_async_wait":
+            dist.all_reduce(x, op=dist.ReduceOp.AVG, async_op=True).wait()
+        elif case == "reduce_scatter_async_wait":
+            dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG, async_op=True).wait()
         elif case == "reduce_scatter_coalesced":
             with dist._coalescing_manager(async_ops=True) as cm:
                 for o, i in zip(outs, xs):
