@@ -8,7 +8,8 @@ import subprocess
 import sys
 
 CASES = ["all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor", "all_gather_coalesced", "reduce_scatter_coalesced",
-         "all_gather_inplace", "reduce_scatter_inplace", "all_reduce_async_wait", "reduce_scatter_async_wait"]
+         "all_gather_inplace", "reduce_scatter_inplace", "all_reduce_async_wait", "reduce_scatter_async_wait",
+         "side_stream_rs", "autograd_rs", "autograd_side_stream_rs"]
 
 
 def child(case):
@@ -21,8 +22,34 @@ def child(case):
     xs = [torch.randn(1 << 18, device="cuda", dtype=torch.bfloat16) for _ in range(3)]
     outs = [torch.empty_like(t) for t in xs]
 
+    def side_rs():
+        s2 = side[0]
+        s2.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s2):
+            dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG, async_op=True).wait()
+        torch.cuda.current_stream().wait_stream(s2)
+
+    class Hook(torch.autograd.Function):      # issues the collective from the autograd thread
+        @staticmethod
+        def forward(ctx, t):
+            return t * 2
+
+        @staticmethod
+        def backward(ctx, g):
+            if case == "autograd_side_stream_rs":
+                side_rs()
+            else:
+                dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG, async_op=True).wait()
+            return g * 2
+    side = [torch.cuda.Stream()]
+    leaf = torch.randn(4096, device="cuda", requires_grad=True)
+
     def run():
-        if case == "all_reduce":
+        if case == "side_stream_rs":
+            side_rs()
+        elif case in ("autograd_rs", "autograd_side_stream_rs"):
+            Hook.apply(leaf).sum().backward()
+        elif case == "all_reduce":
             dist.all_reduce(x, op=dist.ReduceOp.AVG)
         elif case == "reduce_scatter_tensor":
             dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG)
@@ -65,13 +92,16 @@ def main():
     if len(sys.argv) > 2 and sys.argv[1] == "--child":
         child(sys.argv[2])
         return
-    for i, case in enumerate(CASES):
+    for i, case in enumerate(sys.argv[1:] or CASES):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29600 + i))
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", case], env=env,
                            capture_output=True, text=True, timeout=120)
         ok = r.returncode == 0 and "captured_and_replayed" in r.stdout
         print(json.dumps({"case": case, "ok": ok, "returncode": r.returncode,
                           "err": "" if ok else r.stderr.strip().splitlines()[-1][:200] if r.stderr.strip() else ""}), flush=True)
+        if r.returncode < 0 or r.returncode >= 128:   # a crashed child: start nothing more on the GPU
+            print(json.dumps({"stopped_after": r.returncode}), flush=True)
+            sys.exit(3)
 
 
 if __name__ == "__main__":

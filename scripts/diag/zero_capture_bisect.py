@@ -11,6 +11,9 @@ VARIANTS = {
     "s1_fwd_bwd_only": {"stage": 1, "_part": "fb"},
     "s1_step_only": {"stage": 1, "_part": "step"},
     "s1_fwd_only": {"stage": 1, "_part": "f"},
+    "s1_fwd_bwd_nostream": {"stage": 1, "_part": "fb", "_nostream": True},
+    "s1_step_only_nostream": {"stage": 1, "_part": "step", "_nostream": True},
+    "s2_nostream": {"stage": 2, "_nostream": True},
     "s1": {"stage": 1},
     "s2": {"stage": 2},
     "s2_no_overlap_comm": {"stage": 2, "overlap_comm": False},
@@ -32,9 +35,12 @@ def child(name):
     z = {"reduce_bucket_size": 100000, "world1_replicated": False, "force_collectives": True}
     z.update(VARIANTS[name])
     part = z.pop("_part", "all")
+    nostream = z.pop("_nostream", False)
     model = build_model("causal-tiny", dtype=torch.bfloat16, device="cuda", seed=3)
     cfg = {"optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "zero_optimization": z}
     eng, _, _, _ = initialize(model=model, model_parameters=model.parameters(), config=cfg)
+    if nostream:                                # collectives on the capturing stream itself
+        eng.comm_stream = None
     ds = SyntheticLMDataset(model.cfg, 4 * 4, seq_len=128, mlm=False, seed=5)
     ids, lab = ds.input_ids.view(4, 4, 128).cuda(), ds.labels.view(4, 4, 128).cuda()
 
@@ -74,13 +80,17 @@ def main():
     if len(sys.argv) > 2 and sys.argv[1] == "--child":
         child(sys.argv[2])
         return
-    for i, name in enumerate(VARIANTS):
+    names = sys.argv[1:] or list(VARIANTS)
+    for i, name in enumerate(names):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29700 + i), DTD_ZERO_ALLOW_CAPTURE="1")
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", name], env=env,
                            capture_output=True, text=True, timeout=150)
         ok = r.returncode == 0 and '"ok": true' in r.stdout
         tail = "" if ok else " | ".join(r.stderr.strip().splitlines()[-3:])[:400]
         print(json.dumps({"variant": name, "ok": ok, "returncode": r.returncode, "err": tail}), flush=True)
+        if r.returncode < 0 or r.returncode >= 128:   # a crashed child: start nothing more on the GPU
+            print(json.dumps({"stopped_after": r.returncode}), flush=True)
+            sys.exit(3)
 
 
 if __name__ == "__main__":
