@@ -246,6 +246,15 @@ def _ffn_gemm_ok(c, x: torch.Tensor, w: torch.Tensor, *more) -> bool:
             and G.supported(x.shape[0], w.shape[0], x.shape[1], x, w, *more))
 
 
+def _proj_ln(inp, w, bias, res, gamma, beta, eps, p, rng, sid, store_z):
+    """Post-LN sublayer output: LN(res + dropout(inp @ w.T + bias)) -> (z, out, mean, rstd).  One
+    kernel (projection GEMM with the LayerNorm in its epilogue, ops/csrc/gemm_ln.hip) when enabled
+    (DTD_GEMM_LN=1) and the shape tiles; else the Linear, then the fused residual/dropout/LN pass."""
+    if G.ln_fused_enabled() and G.linear_ln_supported(inp, w, res, bias, gamma, beta):
+        return G.linear_ln(inp, w, bias, res, gamma, beta, eps, p, rng, sid, store_z=store_z)
+    return Fx.ln_fwd(G.linear_any(inp, w, bias), res, gamma, beta, eps, p, rng, sid, store_z=store_z)
+
+
 class _FusedLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, layer: TransformerLayer, *params):
@@ -275,12 +284,12 @@ class _FusedLayerFn(torch.autograd.Function):
             a_in = x2d
         qkv = G.linear_any(a_in, qkv_w, qkv_b)
         actx, lse, amask = A.attn_fwd(qkv, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, masks=pend)
-        o = G.linear_any(actx, o_w, o_b)
         ln_fo = _LN_MEMEFF[0] and not c.pre_ln
         if c.pre_ln:
+            o = G.linear_any(actx, o_w, o_b)
             z1, f_in, m2, r2 = Fx.ln_fwd(o, x2d, g2, b2, eps, p_h, rng, s1)
         else:
-            z1, f_in, m1, r1 = Fx.ln_fwd(o, x2d, g1, b1, eps, p_h, rng, s1, store_z=not ln_fo)
+            z1, f_in, m1, r1 = _proj_ln(actx, o_w, o_b, x2d, g1, b1, eps, p_h, rng, s1, store_z=not ln_fo)
         ffn_g = False   # u holds act'(pre-activation) instead of the pre-activation
         if G.ffn_fwd_enabled() and _ffn_gemm_ok(c, f_in, w1):
             if rt.keep_ffn_act and c.activation in G.GRAD_ACTS and G.ffn_store_grad_enabled():
@@ -293,12 +302,12 @@ class _FusedLayerFn(torch.autograd.Function):
         else:
             u = G.linear_any(f_in, w1, bf1)
             a = Fx.act_fwd(u, c.activation)
-        y = G.linear_any(a, w2, bf2)
         if c.pre_ln:
+            y = G.linear_any(a, w2, bf2)
             out = Fx.dropout_add(y, z1, p_h, rng, s2)
             z2 = m3 = r3 = None
         else:
-            z2, out, m3, r3 = Fx.ln_fwd(y, f_in, g2, b2, eps, p_h, rng, s2, store_z=not ln_fo)
+            z2, out, m3, r3 = _proj_ln(a, w2, bf2, f_in, g2, b2, eps, p_h, rng, s2, store_z=not ln_fo)
         a_keep = a if rt.keep_ffn_act else None
         if c.pre_ln:
             ctx.save_for_backward(x2d, a_in, qkv, actx, lse, z1, f_in, u, m1, r1, m2, r2, a_keep)

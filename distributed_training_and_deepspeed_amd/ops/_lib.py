@@ -92,6 +92,9 @@ _SIGS = {
     "dtd_gemm_f32_nt": (I, [P, I, P, I, P, I, P, I, I, I, P]),
     "dtd_gemm_f32_tn_splits": (I, [I, I, I]),
     "dtd_gemm_f32_tn": (I, [P, I, P, I, P, I, I, I, I, P]),
+    # gemm_ln.hip
+    "dtd_gemm_ln_supported": (I, [I, I, I, I, I, I, I]),
+    "dtd_gemm_ln": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, U32, P]),
     # reduce.hip
     "dtd_splitk_reduce": (I, [P, I, I, ctypes.c_longlong, P, I, I, P]),
 }

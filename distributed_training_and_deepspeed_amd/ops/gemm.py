@@ -172,6 +172,49 @@ def set_enabled(on: bool) -> None:
     _ENABLED[0] = bool(on)
 
 
+# Projection GEMM + bias + hidden dropout + residual + LayerNorm in one kernel (ops/csrc/gemm_ln.hip)
+# for the post-LN output sublayers (attention output, FFN output) at hidden size 768.
+_LN_FUSED = [os.environ.get("DTD_GEMM_LN", "0") == "1"]
+
+
+def set_ln_fused(on: bool) -> None:
+    _LN_FUSED[0] = bool(on)
+
+
+def ln_fused_enabled() -> bool:
+    return _LN_FUSED[0]
+
+
+def linear_ln_supported(x: torch.Tensor, w: torch.Tensor, r: torch.Tensor, *vecs) -> bool:
+    """Shape / layout contract of ``linear_ln``: bf16, 16-byte aligned rows, N = 768, M % 128 == 0."""
+    if not (_ok(x) and _ok(w) and _ok(r) and _lib.has("dtd_gemm_ln")):
+        return False
+    if not all(v is None or (v.is_cuda and v.dtype == torch.bfloat16 and v.is_contiguous()
+                             and v.data_ptr() % 16 == 0) for v in vecs):
+        return False
+    M, K = x.shape
+    return (w.shape[1] == K and r.shape == (M, w.shape[0]) and
+            bool(_lib.lib().dtd_gemm_ln_supported(M, w.shape[0], K, x.stride(0), w.stride(0), r.stride(0),
+                                                   w.shape[0])))
+
+
+def linear_ln(x, w, b, r, gamma, beta, eps: float, p: float, rng, sid: int, store_z: bool = False):
+    """``out = LayerNorm(r + dropout(x @ w.T + b))`` in one kernel; the dropout keep law and the
+    (z, out, mean, rstd) result of ``ops.functional.ln_fwd(x @ w.T + b, r, ...)``, with the projection
+    output rounded to bf16 once, as a stored Linear output would be."""
+    M = x.shape[0]
+    N = w.shape[0]
+    out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    z = torch.empty_like(out) if store_z else None
+    mean = torch.empty(M, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    _lib.call("dtd_gemm_ln", x.data_ptr(), w.data_ptr(), _lib.ptr(b), r.data_ptr(), gamma.data_ptr(),
+              beta.data_ptr(), out.data_ptr(), _lib.ptr(z), mean.data_ptr(), rstd.data_ptr(), M, N, x.shape[1],
+              x.stride(0), w.stride(0), r.stride(0), N, float(eps), float(p), rng.state.data_ptr(), sid,
+              _lib.stream())
+    return z, out, mean, rstd
+
+
 def _ok(t: torch.Tensor) -> bool:
     return (t is not None and t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1
             and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0)
