@@ -25,6 +25,7 @@
 // (row >> 2) & 3 (the source address carries the swizzle; every ds_read_b128 fragment read of 32
 // rows at one chunk is bank-conflict free).  One barrier per K-step; the next K-step's first
 // fragments are read right after it, under the current K-step's second half of MFMAs.
+#include <stdlib.h>
 #include <type_traits>
 
 #include "common.h"
@@ -64,6 +65,14 @@ __device__ __forceinline__ void mfma_acc(f32x16& acc, bf16x8 a, bf16x8 b) {
   if constexpr (F < 4) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
   else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
+template <int I, int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  if constexpr (I < N) {
+    fn(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(fn);
+  }
+}
+
 // keep a tile's values in its register file (the epilogue rewrites the accumulators in place)
 template <int F>
 __device__ __forceinline__ void pin(f32x16& acc) {
@@ -101,7 +110,12 @@ __device__ __forceinline__ bf16x4 cvt4(float a, float b, float c, float d) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3);
 }
 
-template <bool DROP, bool BIAS, bool STORE_Z>
+// PIPE = 0: per K-step, DMA issue and fragment reads up front, MFMAs, barrier (simple form).
+// PIPE = 1: the memory instructions ride in the MFMA gaps (sched_barrier-pinned): the second
+// half-step's fragments are read under the first half's MFMAs, and the barrier sits after the
+// first 12 MFMAs of the second half, so the next K-step's first fragments and the DMA of the
+// panels two steps ahead issue under its last 12 -- the matrix pipe never drains at the barrier.
+template <bool DROP, bool BIAS, bool STORE_Z, int PIPE>
 __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -171,6 +185,53 @@ __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
   bar();
   read_frags(0, c0, wa, xa);
 
+  if constexpr (PIPE == 1) {
+    // one 16-row DMA instruction / one fragment read, by index
+    auto dma_one = [&](int j, int kw, int sw, int kx, int sx) {
+      if (j < W_DMA)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(wl + sw * W_STAGE + j * 16 * ROWB), 16, vw,
+                                                 j * sw16 + kw * ROWB, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void*)(xl + sx * X_STAGE + (j - W_DMA) * 16 * ROWB), 16,
+                                                 vx, (j - W_DMA) * sx16 + kx * ROWB, 0, 0);
+    };
+    auto read_one = [&](int j, int kt2, int c, bf16x8 (&wf)[FB], bf16x8 (&xf)[TB]) {
+      if (j < TB) xf[j] = *reinterpret_cast<const bf16x8*>(xfr + (kt2 % 3) * X_STAGE + c + j * 32 * ROWB);
+      else wf[j - TB] = *reinterpret_cast<const bf16x8*>(wfr + (kt2 & 1) * W_STAGE + c + (j - TB) * 32 * ROWB);
+    };
+    // the panels "issued after barrier B(-1)": W(1), X(2)
+    dma_w(min(1, nk - 1), 1);
+    dma_x(min(2, nk - 1), 2);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int kw = min(kt + 2, nk - 1), kx = min(kt + 3, nk - 1), sw = kt & 1, sx = kt % 3;
+      // first half-step: MFMAs on (wa, xa); the second half's 10 fragment reads in gaps 0-9
+      static_for<0, TB * FB>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, t = j / FB, f = j % FB;
+        mfma_acc<f>(acc[t][f], wa[f], xa[t]);
+        if constexpr (j < TB + FB) read_one(j, kt, c1, wb, xb);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      // second half-step: 12 MFMAs, barrier B(kt) (W(kt+1), X(kt+1) landed; stage kt read out),
+      // 12 MFMAs with the next K-step's first fragments and the DMA of W(kt+2), X(kt+3) in the gaps
+      static_for<0, TB * FB>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, t = j / FB, f = j % FB;
+        if constexpr (j == TB * FB / 2) {
+          asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+          bar();
+        }
+        mfma_acc<f>(acc[t][f], wb[f], xb[t]);
+        if constexpr (j >= TB * FB / 2) {
+          constexpr int g0 = 2 * (j - TB * FB / 2);   // memory ops g0, g0 + 1 of 24
+#pragma unroll
+          for (int u = g0; u < g0 + 2; ++u) {
+            if (u < TB + FB) read_one(u, kt + 1, c0, wa, xa);
+            else dma_one(u - (TB + FB), kw, sw, kx, sx);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+  } else
   for (int kt = 0; kt < nk; ++kt) {
     // the next weight panel and the activation panel two K-steps ahead (clamped re-loads of the
     // last panel keep the issue and the counted waits unconditional; their stages are not read)
@@ -305,13 +366,20 @@ DTD_EXPORT int dtd_gemm_ln(const void* x, const void* w, const void* bias, const
                (const bf16*)beta, (bf16*)out, (bf16*)z, mean, rstd, M, K, ldx, ldw, ldr, ldo, eps, p, rng, sid};
   const dim3 grid(M / BM), block(256);
   const bool d = p > 0.f, b = bias != nullptr, zz = z != nullptr;
-  if (d && b && !zz) hipLaunchKernelGGL((gemm_ln_kernel<true, true, false>), grid, block, 0, s, a);
-  else if (d && b) hipLaunchKernelGGL((gemm_ln_kernel<true, true, true>), grid, block, 0, s, a);
-  else if (!d && b && !zz) hipLaunchKernelGGL((gemm_ln_kernel<false, true, false>), grid, block, 0, s, a);
-  else if (!d && b) hipLaunchKernelGGL((gemm_ln_kernel<false, true, true>), grid, block, 0, s, a);
-  else if (d && !zz) hipLaunchKernelGGL((gemm_ln_kernel<true, false, false>), grid, block, 0, s, a);
-  else if (d) hipLaunchKernelGGL((gemm_ln_kernel<true, false, true>), grid, block, 0, s, a);
-  else if (!zz) hipLaunchKernelGGL((gemm_ln_kernel<false, false, false>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((gemm_ln_kernel<false, false, true>), grid, block, 0, s, a);
+  static const int pipe = [] { const char* e = getenv("DTD_GEMM_LN_PIPE"); return e ? atoi(e) : 1; }();
+#define DTD_GLN(D, B, Z)                                                                              \
+  do {                                                                                                \
+    if (pipe) hipLaunchKernelGGL((gemm_ln_kernel<D, B, Z, 1>), grid, block, 0, s, a);                \
+    else hipLaunchKernelGGL((gemm_ln_kernel<D, B, Z, 0>), grid, block, 0, s, a);                     \
+  } while (0)
+  if (d && b && !zz) DTD_GLN(true, true, false);
+  else if (d && b) DTD_GLN(true, true, true);
+  else if (!d && b && !zz) DTD_GLN(false, true, false);
+  else if (!d && b) DTD_GLN(false, true, true);
+  else if (d && !zz) DTD_GLN(true, false, false);
+  else if (d) DTD_GLN(true, false, true);
+  else if (!zz) DTD_GLN(false, false, false);
+  else DTD_GLN(false, false, true);
+#undef DTD_GLN
   DTD_LAUNCH_CHECK();
 }

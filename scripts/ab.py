@@ -95,6 +95,7 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "attn_bwd_fused": _env(DTD_ATTN_BWD="fused"),
            "b320": lambda: ["--batch-size", "320"], "b384": lambda: ["--batch-size", "384"],
            "dkdv_occ1": _env(DTD_ATTN_OCC="3,1,3"),
+           "gemm_ln": _env(DTD_GEMM_LN="1"), "gemm_ln_p0": _env(DTD_GEMM_LN="1", DTD_GEMM_LN_PIPE="0"),
            "base_so": _env(DTD_KERNELS_SO=os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops",
                                                       "_dtd_kernels_base.so"))}
 
