@@ -177,6 +177,65 @@ __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
       mfma_acc<5>(acc[t][5], wf[5], xf[t]);
     }
   };
+  if constexpr (PIPE == 2) {
+    // The weight rows are private to the wave: their MFMA A fragments come straight from global
+    // memory (L2) into registers -- lane l reads row 32 f + (l & 31), 8 k-values at 8 (l >> 5) --
+    // with no LDS round trip and no LDS-DMA (whose issue cost, 60-185 cycles per 1 KiB piece inside
+    // an MFMA stream, bounded the PIPE 0/1 forms at ~3.7k cycles per K-step).  Only the shared
+    // activation panel goes through LDS (3-deep ring, 2 DMA pieces per wave per K-step).  The half
+    // K-step's weight fragments load one half-step ahead: wb under the ks0 MFMAs, wa (next K-step)
+    // under the first ks1 MFMAs.
+    const int vwf = ((lane & 31) * g.ldw + (lane >> 5) * 8) * 2;
+    const int swf = 32 * g.ldw * 2;   // bytes per 32 weight rows
+    auto load_w = [&](int j, int kt2, int ks, bf16x8 (&wf)[FB]) {
+      wf[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, vwf, j * swf + kt2 * ROWB + ks * 32, 0));
+    };
+    auto read_x = [&](int j, int kt2, int c, bf16x8 (&xf)[TB]) {
+      xf[j] = *reinterpret_cast<const bf16x8*>(xfr + (kt2 % 3) * X_STAGE + c + j * 32 * ROWB);
+    };
+    auto dma_x_one = [&](int j, int kx, int sx) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void*)(xl + sx * X_STAGE + j * 16 * ROWB), 16, vx,
+                                               j * sx16 + kx * ROWB, 0, 0);
+    };
+    // prologue: X(0), X(1), X(2) and the first half-step's weight fragments in flight
+    dma_x(0, 0);
+    dma_x(min(1, nk - 1), 1);
+    dma_x(min(2, nk - 1), 2);
+#pragma unroll
+    for (int j = 0; j < FB; ++j) load_w(j, 0, 0, wa);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");   // X(0) landed (own rows)
+    bar();
+#pragma unroll
+    for (int j = 0; j < TB; ++j) read_x(j, 0, c0, xa);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int kn = min(kt + 1, nk - 1), kx = min(kt + 3, nk - 1), sx = kt % 3;
+      static_for<0, TB * FB>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, t = j / FB, f = j % FB;
+        mfma_acc<f>(acc[t][f], wa[f], xa[t]);
+        if constexpr (j < FB) load_w(j, kt, 1, wb);
+        else if constexpr (j < FB + TB) read_x(j - FB, kt, c1, xb);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      static_for<0, TB * FB>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, t = j / FB, f = j % FB;
+        if constexpr (j == TB * FB / 2) {
+          // B(kt): X(kt+1) landed for every wave -- at most the 20 youngest vector-memory ops may
+          // still fly (steady state: wa(kt+1) 6, wb(kt) 6, X(kt+2) 2, wa(kt) 6; X(kt+1) is older)
+          // -- and every wave has read stage kt out
+          asm volatile("s_waitcnt vmcnt(20) lgkmcnt(0)" ::: "memory");
+          bar();
+        }
+        mfma_acc<f>(acc[t][f], wb[f], xb[t]);
+        // gaps 0-5: the next K-step's first-half weight fragments (a half-step of flight before
+        // their MFMAs); after the barrier: its first activation fragments, then the DMA of X(kt+3)
+        if constexpr (j < FB) load_w(j, kn, 0, wa);
+        else if constexpr (j >= TB * FB / 2 && j < TB * FB / 2 + TB) read_x(j - TB * FB / 2, kt + 1, c0, xa);
+        else if constexpr (j >= TB * FB / 2 + TB && j < TB * FB / 2 + TB + X_DMA)
+          dma_x_one(j - TB * FB / 2 - TB, kx, sx);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+  } else {
   // prologue: W(0), X(0), X(1) issued; W(0) and X(0) landed
   dma_w(0, 0);
   dma_x(0, 0);
@@ -245,6 +304,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
     bar();
     if (kt + 1 < nk) read_frags(kt + 1, c0, wa, xa);
   }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // acc_settle: 16 wait states for the last MFMAs' results (8-pass XDL needs 12 before a VALU or
   // v_accvgpr_read touches them), then pin every tile in its file so no read is hoisted above
@@ -271,6 +331,12 @@ __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
   const uint32_t thr = keep_threshold(g.p);
   const float dscale = DROP ? 1.f / (1.f - g.p) : 1.f;
   const int sub = lane & 31, rsel = lane >> 5;
+  bf16x8 gm8[3], bt8[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    gm8[c] = *reinterpret_cast<const bf16x8*>(g.gamma + (c * 32 + sub) * 8);
+    bt8[c] = *reinterpret_cast<const bf16x8*>(g.beta + (c * 32 + sub) * 8);
+  }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     // accumulators of token tiles 2 half, 2 half + 1 -> LDS (bias added in fp32, one rounding)
@@ -290,19 +356,34 @@ __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
         }
     }
     bar();
-    // LayerNorm of the 64 rows: wave w takes rows 16 w .. 16 w + 15, two per step
+    // LayerNorm of the 64 rows: wave w takes rows 16 w .. 16 w + 15, two per step.  One wave per
+    // SIMD hides no memory latency by itself: the residual rows of the next step are loaded while
+    // this step computes.
+    auto load_r = [&](int rp, bf16x8 (&rv)[3]) {
+      const int row = m0 + half * 64 + w * 16 + 2 * rp + rsel;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        rv[c] = *reinterpret_cast<const bf16x8*>(g.r + (size_t)row * g.ldr + (c * 32 + sub) * 8);
+    };
+    bf16x8 rnext[3];
+    load_r(0, rnext);
 #pragma unroll 1
     for (int rp = 0; rp < 8; ++rp) {
       const int lr = w * 16 + 2 * rp + rsel;          // row within the half
       const int row = m0 + half * 64 + lr;
       const size_t base = (size_t)row * NH;
+      bf16x8 rcur[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) rcur[c] = rnext[c];
+      if (rp + 1 < 8) load_r(rp + 1, rnext);
       float z[24];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const int col = (c * 32 + sub) * 8;
         const bf16x8 y8 = *reinterpret_cast<const bf16x8*>(smem + lr * YP + col * 2);
         float rr[8];
-        vload<bf16, 8>(g.r + (size_t)row * g.ldr + col, rr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rr[j] = (float)rcur[c][j];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float y = (float)y8[j];
@@ -332,11 +413,9 @@ __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const int col = (c * 32 + sub) * 8;
-        float o[8], gm[8], bt[8];
-        vload<bf16, 8>(g.gamma + col, gm);
-        vload<bf16, 8>(g.beta + col, bt);
+        float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (z[8 * c + j] - mu) * rs * gm[j] + bt[j];
+        for (int j = 0; j < 8; ++j) o[j] = (z[8 * c + j] - mu) * rs * (float)gm8[c][j] + (float)bt8[c][j];
         vstore<bf16, 8>(g.out + (size_t)row * g.ldo + col, o);
       }
     }
@@ -366,10 +445,11 @@ DTD_EXPORT int dtd_gemm_ln(const void* x, const void* w, const void* bias, const
                (const bf16*)beta, (bf16*)out, (bf16*)z, mean, rstd, M, K, ldx, ldw, ldr, ldo, eps, p, rng, sid};
   const dim3 grid(M / BM), block(256);
   const bool d = p > 0.f, b = bias != nullptr, zz = z != nullptr;
-  static const int pipe = [] { const char* e = getenv("DTD_GEMM_LN_PIPE"); return e ? atoi(e) : 1; }();
+  static const int pipe = [] { const char* e = getenv("DTD_GEMM_LN_PIPE"); return e ? atoi(e) : 2; }();
 #define DTD_GLN(D, B, Z)                                                                              \
   do {                                                                                                \
-    if (pipe) hipLaunchKernelGGL((gemm_ln_kernel<D, B, Z, 1>), grid, block, 0, s, a);                \
+    if (pipe == 2) hipLaunchKernelGGL((gemm_ln_kernel<D, B, Z, 2>), grid, block, 0, s, a);           \
+    else if (pipe) hipLaunchKernelGGL((gemm_ln_kernel<D, B, Z, 1>), grid, block, 0, s, a);           \
     else hipLaunchKernelGGL((gemm_ln_kernel<D, B, Z, 0>), grid, block, 0, s, a);                     \
   } while (0)
   if (d && b && !zz) DTD_GLN(true, true, false);
