@@ -602,9 +602,20 @@ class ZeroEngine(nn.Module):
             elif not s.launched:
                 self._reduce_segment(s)
 
+    def _capturing(self) -> bool:
+        return self.cuda and torch.cuda.is_current_stream_capturing()
+
+    def _cs(self):
+        """The comm stream, or None while a hipGraph capture is in progress: a collective issued on
+        a side stream joined to the capture crashed hipStreamEndCapture on the box (RCCL
+        reduce-scatter, scripts/diag/capture_collectives.py side_stream_rs) while the same
+        collective on the capturing stream itself captures and replays -- inside a graph the
+        collectives run on the capture stream (RCCL still launches them on its own stream)."""
+        return None if self._capturing() else self.comm_stream
+
     def _comm_ctx(self, stream=None):
         stream = stream if stream is not None else self.comm_stream
-        if stream is None:
+        if stream is None or self._capturing():
             return contextlib.nullcontext()
         stream.wait_stream(torch.cuda.current_stream(self.device))
         return torch.cuda.stream(stream)
@@ -645,12 +656,13 @@ class ZeroEngine(nn.Module):
                     out.add_(dst)
             ev = None
             landed = (self.stage >= 2 and not self.replicated) or s.unit
-            if self.comm_stream is not None and landed:
+            cs = self._cs()
+            if cs is not None and landed:
                 ev = torch.cuda.Event()
-                ev.record(self.comm_stream)
+                ev.record(cs)
         if landed:
             if not (s.unit and self.alias_units):
-                self.landing.release(buf, ev, self.comm_stream)
+                self.landing.release(buf, ev, cs)
             s.gbuf = None
             for p in s.params:
                 p.main_grad = None
@@ -671,7 +683,7 @@ class ZeroEngine(nn.Module):
             if not s.launched:
                 self._reduce_unit(s)
         self._release_pending()
-        if self.comm_stream is not None:
+        if self._cs() is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
 
     # ================================================================== stage 3 units
@@ -696,7 +708,7 @@ class ZeroEngine(nn.Module):
                 w.wait()
             else:
                 full.copy_(src)
-            if self.gather_stream is not None:
+            if self.gather_stream is not None and not self._capturing():
                 ev = torch.cuda.Event()
                 ev.record(self.gather_stream)
                 s.gather_event = ev
@@ -836,7 +848,7 @@ class ZeroEngine(nn.Module):
             self.micro_step += 1
             self._need_reset = True
             return
-        if self.comm_stream is not None:
+        if self._cs() is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
         self.optimizer.step()
         self._refresh_params()
@@ -874,12 +886,12 @@ class ZeroEngine(nn.Module):
                 else:
                     for o, i in zip(outs, ins):
                         o.copy_(i)
-                if self.comm_stream is not None and not wait:
+                if self._cs() is not None and not wait:
                     ev = torch.cuda.Event()
                     ev.record(self.comm_stream)
                     for s in grp:
                         self._refresh_events[s.index] = ev
-        if self.comm_stream is not None and wait:
+        if self._cs() is not None and wait:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
 
     def zero_optimization_stage(self) -> int:

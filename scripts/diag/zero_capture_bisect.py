@@ -16,6 +16,7 @@ VARIANTS = {
     "s2_nostream": {"stage": 2, "_nostream": True},
     "s1": {"stage": 1},
     "s2": {"stage": 2},
+    "s3": {"stage": 3},
     "s2_no_overlap_comm": {"stage": 2, "overlap_comm": False},
     "s2_no_refresh_overlap": {"stage": 2, "overlap_param_refresh": False},
     "s2_neither": {"stage": 2, "overlap_comm": False, "overlap_param_refresh": False},
