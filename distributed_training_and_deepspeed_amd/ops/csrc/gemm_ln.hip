@@ -445,7 +445,7 @@ DTD_EXPORT int dtd_gemm_ln(const void* x, const void* w, const void* bias, const
                (const bf16*)beta, (bf16*)out, (bf16*)z, mean, rstd, M, K, ldx, ldw, ldr, ldo, eps, p, rng, sid};
   const dim3 grid(M / BM), block(256);
   const bool d = p > 0.f, b = bias != nullptr, zz = z != nullptr;
-  static const int pipe = [] { const char* e = getenv("DTD_GEMM_LN_PIPE"); return e ? atoi(e) : 2; }();
+  static const int pipe = [] { const char* e = getenv("DTD_GEMM_LN_PIPE"); return e ? atoi(e) : 1; }();
 #define DTD_GLN(D, B, Z)                                                                              \
   do {                                                                                                \
     if (pipe == 2) hipLaunchKernelGGL((gemm_ln_kernel<D, B, Z, 2>), grid, block, 0, s, a);           \
