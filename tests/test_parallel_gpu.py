@@ -67,6 +67,42 @@ def test_zero_rccl_collectives_at_world1_match_local_path(rccl_world1, stage):
     assert torch.equal(ml, mf)
 
 
+def _ddp_run(force, steps=4, overlap=True):
+    """bench.py's data path at small scale: fused BERT, DDP buckets (shaped tail buckets), fused
+    AdamW with the stage-by-stage update overlapped with the next forward."""
+    from distributed_training_and_deepspeed_amd.optim import hf_adamw
+    from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
+    model = build_model("tiny", dtype=torch.bfloat16, device="cuda", seed=3)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=0.25, force_collectives=force)
+    opt = hf_adamw(ddp.parameters(), lr=1e-3)
+    if overlap:
+        opt.overlap_with_forward(model.zero3_units(), root=model)
+    ds = SyntheticLMDataset(model.cfg, 4 * steps, seq_len=128, seed=1)
+    ids, lab = ds.input_ids.view(steps, 4, 128).cuda(), ds.labels.view(steps, 4, 128).cuda()
+    losses = []
+    for i in range(steps):
+        out = ddp(ids[i], labels=lab[i])
+        out.loss.backward()
+        opt.step()
+        model.rt.rng.advance()
+        losses.append(out.loss.detach())
+    opt.synchronize()
+    torch.cuda.synchronize()
+    return [x.item() for x in losses], [p.detach().clone() for p in model.parameters()], ddp
+
+
+def test_ddp_rccl_bucket_allreduce_with_optimizer_overlap_matches_local_path(rccl_world1):
+    """The N > 1 step of bench.py on one GPU: every bucket's RCCL all-reduce (AVG over one rank
+    is exact) issued from the autograd thread, the optimizer's stage-by-stage update on its side
+    stream under the next forward -- bitwise equal to the same step without collectives."""
+    ll, pl, dl = _ddp_run(False)
+    lf, pf, df = _ddp_run(True)
+    assert df.collectives and not dl.collectives and len(df.buckets) > 2
+    assert ll == lf, (ll, lf)
+    for a, b in zip(pl, pf):
+        assert torch.equal(a, b)
+
+
 def test_gpipe_two_stages_one_gpu_recompute_is_exact():
     from distributed_training_and_deepspeed_amd.models.bert_mp import BertModelWithMP
     cfg = C.BERT_TINY
