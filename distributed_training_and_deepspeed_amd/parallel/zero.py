@@ -815,14 +815,6 @@ class ZeroEngine(nn.Module):
         self._need_reset = False
 
     def forward(self, *args, **kwargs):
-        if (self.collect and self.cuda and torch.cuda.is_current_stream_capturing()
-                and os.environ.get("DTD_ZERO_ALLOW_CAPTURE", "0") != "1"):   # (=1: diagnostics only)
-            # measured on the box (tests/test_graph_gpu.py): capturing the ZeRO-2/3 step with its
-            # RCCL reduce-scatters / all-gathers crashes inside hipStreamEndCapture (segfault in
-            # capture_end), while a captured DDP step with RCCL all-reduces replays correctly --
-            # refuse here instead of crashing the process
-            raise RuntimeError("ZeRO steps with RCCL collectives cannot be captured in a hipGraph "
-                               "(hipStreamEndCapture crashes on them); run this engine eagerly")
         if self._need_reset:
             self._reset()
         if self._refresh_events and self.cuda and torch.cuda.is_current_stream_capturing():

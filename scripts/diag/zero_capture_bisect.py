@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Bisect the ZeRO capture crash with RCCL collectives (world 1, force_collectives): each variant
-captures a causal-tiny ZeRO step in its own child process with DTD_ZERO_ALLOW_CAPTURE=1 and
-reports whether capture + replay survive."""
+captures a causal-tiny ZeRO step in its own child process and reports whether capture + replay
+survive (variants *_nostream drop the comm stream by hand; the engine now does that itself while
+capturing -- every variant passed on the box, profiles/r4_s12_results.jsonl)."""
 import json
 import os
 import subprocess
@@ -83,7 +84,7 @@ def main():
         return
     names = sys.argv[1:] or list(VARIANTS)
     for i, name in enumerate(names):
-        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29700 + i), DTD_ZERO_ALLOW_CAPTURE="1")
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29700 + i))
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", name], env=env,
                            capture_output=True, text=True, timeout=150)
         ok = r.returncode == 0 and '"ok": true' in r.stdout

@@ -158,11 +158,12 @@ def test_mp_script_graph_trains_like_eager(mode):
 @pytest.mark.parametrize("engine", ["ddp", "zero2", "zero3"])
 def test_captured_step_with_rccl_collectives_matches_eager(engine):
     """The N > 1 data path inside a hipGraph: force_collectives makes DDP issue its bucket
-    all-reduces (RCCL, from the autograd thread, on RCCL's stream) at world 1; the captured step
-    (collectives included) replays exactly like the eager one.  rocprofv3 of bench.py
-    --force-collectives shows the RCCL kernels in the step (profiles/r4_force_collectives_kernels.txt).
-    ZeRO-2/3 with their reduce-scatters / all-gathers crashed inside hipStreamEndCapture on the box:
-    the engine refuses the capture with an error instead (checked here)."""
+    all-reduces (RCCL, from the autograd thread, on RCCL's stream) at world 1, ZeRO-2/3 their
+    reduce-scatters and refresh all-gathers; the captured step (collectives included) replays
+    exactly like the eager one.  rocprofv3 of bench.py --force-collectives shows the RCCL kernels in
+    the step (profiles/r4_force_collectives_kernels.txt).  Inside a capture the ZeRO engine issues
+    its collectives on the capturing stream: on its side comm stream hipStreamEndCapture crashed
+    (scripts/diag/capture_collectives.py side_stream_rs, profiles/r4_s9_results.jsonl)."""
     import os
     from distributed_training_and_deepspeed_amd import comm
     from distributed_training_and_deepspeed_amd.parallel.zero import initialize
@@ -207,10 +208,6 @@ def test_captured_step_with_rccl_collectives_matches_eager(engine):
         lab = ds.labels.view(8, 4, 128).cuda()
         ma, sa = setup()
         mb, sb = setup()
-        if engine != "ddp":
-            with pytest.raises(RuntimeError, match="cannot be captured"):
-                CapturedStep(sb, {"input_ids": ids[0], "labels": lab[0]}, warmup=1, runtime=mb.rt)
-            return
         cap = CapturedStep(sb, {"input_ids": ids[0], "labels": lab[0]}, warmup=3, runtime=mb.rt)
         la = [sa(ids[0], lab[0]) for _ in range(3)]
         la += [sa(ids[i], lab[i]) for i in range(1, 6)]

@@ -48,7 +48,9 @@ def train(model_name, batch_size, training_steps, stage, opts):
     cfg = get_config(model_name)
     model = build_model(model_name, dtype=dtype, device=device, seed=0, impl=opts.impl)
 
-    if opts.graph == "auto":  # multi-rank RCCL capture stays opt-in
+    if opts.graph == "auto":
+        # at world > 1 eager by default: the run's comm-latency report (the comms logger times each
+        # collective) is the script's output; --graph on captures the collectives too (untimed)
         opts.graph = "on" if (cuda and world_size == 1) else "off"
     # every stage is capturable: stage-2/3 gradient landing regions and stage-3 gathered units
     # live in persistent ring arenas (parallel/zero.py _Arena), so replays reuse one address set
