@@ -140,27 +140,38 @@ def test_estimator_matches_allocator_on_gpu():
     assert 0.95 * est <= got <= 1.7 * est, (got, est)
 
 
-def _ddp_gloo_gpu(rank, world, port, out):
+def _ddp_gloo_gpu(rank, world, port, out, bench_like=False):
     from distributed_training_and_deepspeed_amd.optim import hf_adamw
     from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
     comm.init(rank=rank, world_size=world, backend="gloo", init_method=f"file://{out}/rdzv")
     torch.cuda.set_device(0)
-    model = build_model("tiny", dtype=torch.float32, device="cuda:0", seed=3)
+    dt = torch.bfloat16 if bench_like else torch.float32
+    model = build_model("tiny", dtype=dt, device="cuda:0", seed=3)
     ddp = DistributedDataParallel(model, bucket_cap_mb=0.5)
     opt = hf_adamw(ddp.parameters(), lr=1e-3)
+    if bench_like:   # bench.py's N > 1 step: bf16, the optimizer staged under the next forward
+        opt.overlap_with_forward(model.zero3_units(), root=model)
     ds = SyntheticLMDataset(model.cfg, 4, seq_len=64, seed=10 + rank)
-    for _ in range(2):
+    for _ in range(3 if bench_like else 2):
         ddp(ds.input_ids.cuda(), labels=ds.labels.cuda()).loss.backward()
         opt.step()
-    torch.save(next(model.parameters()).detach().cpu(), os.path.join(out, f"p{rank}.pt"))
+        model.rt.rng.advance()
+    if bench_like:
+        opt.synchronize()
+    torch.save([p.detach().cpu() for p in model.parameters()], os.path.join(out, f"p{rank}.pt"))
     comm.destroy()
 
 
-def test_ddp_two_ranks_share_one_gpu_stay_in_sync(tmp_path, free_port):
-    mp.spawn(_ddp_gloo_gpu, args=(2, free_port, str(tmp_path)), nprocs=2, join=True)
+@pytest.mark.parametrize("bench_like", [False, True])
+def test_ddp_two_ranks_share_one_gpu_stay_in_sync(tmp_path, free_port, bench_like):
+    """Two processes share cuda:0 over gloo with different batches: after the gradient all-reduce
+    every parameter is identical on both ranks (an optimizer that read a gradient before its
+    bucket's reduction finished -- e.g. the side-stream staged update -- would diverge)."""
+    mp.spawn(_ddp_gloo_gpu, args=(2, free_port, str(tmp_path), bench_like), nprocs=2, join=True)
     a = torch.load(tmp_path / "p0.pt", weights_only=True)
     b = torch.load(tmp_path / "p1.pt", weights_only=True)
-    assert torch.equal(a, b)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
 
 
 def _zero_gloo_gpu(rank, world, port, out, stage):
