@@ -5,4 +5,5 @@ cd "${GRAFT_REPO_ROOT}"
 source scripts/gpu_step.sh
 export TMPDIR=/tmp
 B=64 step attn_stall 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_VALU_MFMA_BUSY_CYCLES -d gpurun_out/attn_stall -o run --output-format csv -- python scripts/bench_attn.py 3,2,3
+step bench_table 300 python bench.py
 echo done
