@@ -16,6 +16,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 
 from . import _lib
@@ -189,6 +191,9 @@ class PendingMasks:
         self.masks, self.event = masks, event
 
 
+_MASK_REPEAT = max(1, int(os.environ.get("DTD_ATTN_MASK_REPEAT", "1")))
+
+
 def attn_masks_async(B, S, H, D, p, rng: RngState, sid, device) -> PendingMasks | None:
     """Start generating the attention-dropout keep bits on a side stream.  The kernel is pure
     VALU (counter-RNG hashing) and independent of the activations, so issued before the QKV
@@ -202,8 +207,9 @@ def attn_masks_async(B, S, H, D, p, rng: RngState, sid, device) -> PendingMasks 
     side = _side_stream(torch.device(device))
     side.wait_stream(cur)                      # the rng step / previous users of the buffer
     with torch.cuda.stream(side):
-        _lib.call("dtd_attn_masks", masks.data_ptr(), B, S, H, float(p), rng.state.data_ptr(), sid,
-                  side.cuda_stream)
+        for _ in range(_MASK_REPEAT):   # (diagnostic: DTD_ATTN_MASK_REPEAT > 1 prices the generator)
+            _lib.call("dtd_attn_masks", masks.data_ptr(), B, S, H, float(p), rng.state.data_ptr(), sid,
+                      side.cuda_stream)
         ev = torch.cuda.Event()
         ev.record(side)
     return PendingMasks(masks, ev)
