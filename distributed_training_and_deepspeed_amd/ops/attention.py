@@ -15,7 +15,6 @@ attention mask for BERT (data_parallel_training.py:53), so padding is attended t
 from __future__ import annotations
 
 import math
-
 import os
 
 import torch
