@@ -150,25 +150,8 @@ _SIDE = {}
 def _side_stream(device) -> torch.cuda.Stream:
     s = _SIDE.get(device)
     if s is None:
-        cu = os.environ.get("DTD_ATTN_MASK_CU")   # experiment: keep-mask generator on a CU subset
-        s = _SIDE[device] = _cu_masked_stream(device, int(cu, 0)) if cu else torch.cuda.Stream(device)
+        s = _SIDE[device] = torch.cuda.Stream(device)
     return s
-
-
-def _cu_masked_stream(device, word: int):
-    """A HIP stream whose kernels run only on the CUs selected by ``word`` repeated over the CU mask
-    (hipExtStreamCreateWithCUMask, e.g. 0x55555555: every other CU), wrapped for torch."""
-    import ctypes
-    path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
-    hip = ctypes.CDLL(path)
-    n = (torch.cuda.get_device_properties(device).multi_processor_count + 31) // 32
-    mask = (ctypes.c_uint32 * n)(*([word & 0xffffffff] * n))
-    handle = ctypes.c_void_p()
-    with torch.cuda.device(device):
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(n), mask)
-    if rc != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-    return torch.cuda.ExternalStream(handle.value, device=device)
 
 
 def mask_words(B: int, H: int, S: int) -> int:

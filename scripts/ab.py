@@ -80,8 +80,6 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "wgrad_s1": _wgrad_fixed(1), "wgrad_s4": _wgrad_fixed(4), "wgrad_s8": _wgrad_fixed(8),
            "retuned": _env(DTD_TUNED_TABLE=os.path.join(ROOT, "gpurun_out", "tunableop_new0.csv")),
            "mask_x2": _env(DTD_ATTN_MASK_REPEAT="2"),
-           "mask_cu_half": _env(DTD_ATTN_MASK_CU="0x55555555"), "mask_cu_quarter": _env(DTD_ATTN_MASK_CU="0x11111111"),
-           "mask_cu_3q": _env(DTD_ATTN_MASK_CU="0x77777777"),
            "wgrad_s32": _wgrad_fixed(32), "wgrad_s64": _wgrad_fixed(64),
            "gemm_split": _env(DTD_GEMM_VARIANT="2"), "dgrad_nn": _env(DTD_DGRAD_NT="0"),
            "dkdv_bm64": _env(DTD_ATTN_DKDV_BM="64"), "gemm_all": _env(DTD_GEMM_ALL="1"),
