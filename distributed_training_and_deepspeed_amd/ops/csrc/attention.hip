@@ -243,10 +243,6 @@ __device__ __forceinline__ uint32_t swap_stage(uint32_t t, uint32_t sh, uint32_t
   const uint32_t rot = __builtin_amdgcn_alignbit(y, y, sh);
   return (rot & mk) | (t & ~mk);
 }
-// ILP = 2: each wave carries the words kw and kw + 4 together -- two independent xorshift chains
-// interleaved, so the serial shift / xor dependency of one word no longer stalls the issue (the
-// generator alone measured 75 % of its wave cycles issue-stalled, profiles/r4_attn_stall_pmc.json).
-template <int ILP>
 __global__ void __launch_bounds__(256) attn_mask_kernel_t(uint32_t* __restrict__ maskA, uint32_t* __restrict__ maskB,
                                                           int S, int W, const uint64_t* rng, uint32_t sid, uint32_t thr) {
   DropoutRng g(rng, sid);
@@ -267,45 +263,29 @@ __global__ void __launch_bounds__(256) attn_mask_kernel_t(uint32_t* __restrict__
     mk[i] = up ? ~Hs : Hs;
   }
   const int qw = blockIdx.x * 2 + (lane >> 5);   // query word of the B entry this lane stores
-  for (int kw0 = threadIdx.x >> 6; kw0 < W; kw0 += 4 * ILP) {
-    uint32_t x[ILP], word[ILP];
+  for (int kw = threadIdx.x >> 6; kw < W; kw += 4) {
+    uint32_t x = g.bits(ctr0 + kw);
+    x = x ? x : 0x6d2b79f5u;
+    uint32_t word = 0;
 #pragma unroll
-    for (int u = 0; u < ILP; ++u) {
-      const int kw = min(kw0 + 4 * u, W - 1);    // a clamped duplicate past W is computed, not stored
-      x[u] = g.bits(ctr0 + kw);
-      x[u] = x[u] ? x[u] : 0x6d2b79f5u;
-      word[u] = 0;
+    for (int n = 0; n < 16; ++n) {
+      if (n) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; }
+      word = __builtin_amdgcn_alignbit(word, (uint32_t)(thm1 - (int)(x & 0xffffu)), 31);
+      word = __builtin_amdgcn_alignbit(word, (uint32_t)(thm1 - (int)(x >> 16)), 31);
     }
-#pragma unroll
-    for (int n = 0; n < 16; ++n)
-#pragma unroll
-      for (int u = 0; u < ILP; ++u) {
-        if (n) { x[u] ^= x[u] << 13; x[u] ^= x[u] >> 17; x[u] ^= x[u] << 5; }
-        word[u] = __builtin_amdgcn_alignbit(word[u], (uint32_t)(thm1 - (int)(x[u] & 0xffffu)), 31);
-        word[u] = __builtin_amdgcn_alignbit(word[u], (uint32_t)(thm1 - (int)(x[u] >> 16)), 31);
-      }
-#pragma unroll
-    for (int u = 0; u < ILP; ++u) {
-      const int kw = kw0 + 4 * u;
-      uint32_t w = __builtin_bitreverse32(word[u]);
-      const int nk = S - kw * 32;                  // valid keys in this word
-      if (nk < 32) w &= nk > 0 ? (0xffffffffu >> (32 - nk)) : 0u;
-      if (qv && kw < W) maskA[((size_t)bh * W + kw) * (32 * W) + lm_pos(q)] = w;
-      uint32_t t = w;
-      t = swap_stage<16>(t, sh[0], mk[0]);
-      t = swap_stage<8>(t, sh[1], mk[1]);
-      t = swap_stage<4>(t, sh[2], mk[2]);
-      t = swap_stage<2>(t, sh[3], mk[3]);
-      t = swap_stage<1>(t, sh[4], mk[4]);
-      const int key = kw * 32 + (lane & 31);
-      if (kw < W && key < S && qw < W) maskB[((size_t)bh * W + qw) * (32 * W) + lm_pos(key)] = t;
-    }
+    word = __builtin_bitreverse32(word);
+    const int nk = S - kw * 32;                  // valid keys in this word
+    if (nk < 32) word &= (0xffffffffu >> (32 - nk));
+    if (qv) maskA[((size_t)bh * W + kw) * (32 * W) + lm_pos(q)] = word;
+    uint32_t t = word;
+    t = swap_stage<16>(t, sh[0], mk[0]);
+    t = swap_stage<8>(t, sh[1], mk[1]);
+    t = swap_stage<4>(t, sh[2], mk[2]);
+    t = swap_stage<2>(t, sh[3], mk[3]);
+    t = swap_stage<1>(t, sh[4], mk[4]);
+    const int key = kw * 32 + (lane & 31);
+    if (key < S && qw < W) maskB[((size_t)bh * W + qw) * (32 * W) + lm_pos(key)] = t;
   }
-}
-
-static int mask_ilp() {
-  static const int v = [] { const char* e = getenv("DTD_ATTN_MASK_ILP"); return e ? atoi(e) : 1; }();
-  return v;
 }
 
 static bool mask_ballot() {
@@ -1898,7 +1878,7 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
     // stream, overlapping the QKV GEMM)
     if (rng) {
       uint32_t* mB = masks + (size_t)B * H * (32 * W) * W;
-      hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : mask_ilp() == 2 ? attn_mask_kernel_t<2> : attn_mask_kernel_t<1>, dim3((S + 63) / 64, B * H), dim3(256), 0,
+      hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : attn_mask_kernel_t, dim3((S + 63) / 64, B * H), dim3(256), 0,
                          s, mA, mB, S, W, rng, sid, keep_threshold(p));
     }
   }
@@ -1939,7 +1919,7 @@ DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, con
   if (B * S * H == 0 || p <= 0.f) return 0;
   if (!masks || !rng) return (int)hipErrorInvalidValue;
   const int W = (S + 31) / 32;
-  hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : mask_ilp() == 2 ? attn_mask_kernel_t<2> : attn_mask_kernel_t<1>, dim3((S + 63) / 64, B * H), dim3(256), 0, s,
+  hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : attn_mask_kernel_t, dim3((S + 63) / 64, B * H), dim3(256), 0, s,
                      masks, masks + (size_t)B * H * (32 * W) * W, S, W, rng, sid, keep_threshold(p));
   DTD_LAUNCH_CHECK();
 }

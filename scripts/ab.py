@@ -79,7 +79,7 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "attn_occ_322": _env(DTD_ATTN_OCC="3,2,2"), "attn_occ_323_dq64": _env(DTD_ATTN_OCC="3,2,3", DTD_ATTN_TILE="64,64"),
            "wgrad_s1": _wgrad_fixed(1), "wgrad_s4": _wgrad_fixed(4), "wgrad_s8": _wgrad_fixed(8),
            "retuned": _env(DTD_TUNED_TABLE=os.path.join(ROOT, "gpurun_out", "tunableop_new0.csv")),
-           "mask_x2": _env(DTD_ATTN_MASK_REPEAT="2"), "mask_ilp2": _env(DTD_ATTN_MASK_ILP="2"),
+           "mask_x2": _env(DTD_ATTN_MASK_REPEAT="2"),
            "wgrad_s32": _wgrad_fixed(32), "wgrad_s64": _wgrad_fixed(64),
            "gemm_split": _env(DTD_GEMM_VARIANT="2"), "dgrad_nn": _env(DTD_DGRAD_NT="0"),
            "dkdv_bm64": _env(DTD_ATTN_DKDV_BM="64"), "gemm_all": _env(DTD_GEMM_ALL="1"),
