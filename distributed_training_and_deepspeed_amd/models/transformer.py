@@ -18,6 +18,7 @@ model/transformer.py:18-106 (see ``models/transformer_block.py`` for the hookabl
 from __future__ import annotations
 
 import os
+import warnings
 
 import math
 
@@ -59,6 +60,9 @@ class Runtime:
         # Memory-bound runs (max-params ZeRO-3) turn it off.
         self.keep_ffn_act = True
         self.pending_wt: list | None = None   # weights to batch-transpose at the start of the backward
+        # memory-efficient post-LN backward for this model: None follows DTD_LN_MEMEFF; loading a
+        # state dict whose LayerNorms are ill-conditioned for it sets False (ln_memeff_safe)
+        self.ln_memeff: bool | None = None
 
     def new_sid(self) -> int:
         """Dropout stream id for one call site; deterministic per model structure so two
@@ -146,6 +150,8 @@ class TransformerLayer(nn.Module):
         self.sid_attn = rt.new_sid()
         self.sid_1 = rt.new_sid()
         self.sid_2 = rt.new_sid()
+        if not cfg.pre_ln:
+            self.register_load_state_dict_post_hook(_check_loaded_ln)
         # ALiBi slopes stay fp32 (not a buffer, so model.to(bfloat16) does not round them).
         self._alibi = A.alibi_slopes(cfg.num_heads) if cfg.alibi else None
 
@@ -229,6 +235,39 @@ _FUSED_QKV_BIAS = [os.environ.get("DTD_ATTN_QKV_BIAS", "1") == "1"]
 # output, which the layer keeps anyway (fc1's input / the next layer's input).  One [T, h] write
 # per LayerNorm forward and one [T, h] activation per LayerNorm less.
 _LN_MEMEFF = [os.environ.get("DTD_LN_MEMEFF", "1") == "1"]
+# (out - beta) / gamma multiplies the bf16 rounding of out by about |beta| / |gamma|, and a gamma of
+# exactly 0 would leave its column's dgamma at 0 for good.  The recompute is used only while every
+# post-LN column has |gamma| >= max(_LN_GAMMA_FLOOR, |beta| / _LN_BETA_RATIO).  At the ratio limit the
+# recomputed dgamma is within ~1.3 % (relative L2) of the fp32 stored-z one, dx within ~0.1 %
+# (tests/test_models_cpu.py::test_ln_memeff_error_at_the_guard_limit).
+_LN_BETA_RATIO, _LN_GAMMA_FLOOR = 8.0, 1e-3
+
+
+def ln_memeff_safe(layers) -> bool:
+    """True if every post-LN LayerNorm of `layers` is well-conditioned for the memory-efficient
+    backward (x-hat recomputed from the output).  One host sync; run at load time, not per step."""
+    with torch.no_grad():
+        for layer in layers:
+            if layer.cfg.pre_ln:
+                continue
+            for g, b in ((layer.ln1_g, layer.ln1_b), (layer.ln2_g, layer.ln2_b)):
+                if g.numel() == 0 or g.numel() != b.numel():   # released ZeRO-3 shard: no data here
+                    continue
+                lim = torch.clamp(b.detach().float().abs() / _LN_BETA_RATIO, min=_LN_GAMMA_FLOOR)
+                if bool((g.detach().float().abs() < lim).any()):
+                    return False
+    return True
+
+
+def _check_loaded_ln(layer, incompatible_keys) -> None:
+    """load_state_dict post-hook of a post-LN layer: loaded LayerNorm parameters outside the
+    memory-efficient backward's safe range switch the model to the stored-z backward (an explicit
+    rt.ln_memeff is left alone).  The reference's HF LayerNorm always stores its input."""
+    rt = layer.rt
+    if rt.ln_memeff is None and _LN_MEMEFF[0] and not ln_memeff_safe([layer]):
+        rt.ln_memeff = False
+        warnings.warn("post-LN LayerNorm with |gamma| < max(1e-3, |beta|/8) loaded: using the "
+                      "stored-z LayerNorm backward for this model", RuntimeWarning)
 
 
 _dgrad = G.dgrad
@@ -284,7 +323,7 @@ class _FusedLayerFn(torch.autograd.Function):
             a_in = x2d
         qkv = G.linear_any(a_in, qkv_w, qkv_b)
         actx, lse, amask = A.attn_fwd(qkv, B, S, H, D, c.causal, layer.alibi, p_a, rng, sa, masks=pend)
-        ln_fo = _LN_MEMEFF[0] and not c.pre_ln
+        ln_fo = (_LN_MEMEFF[0] if rt.ln_memeff is None else rt.ln_memeff) and not c.pre_ln
         if c.pre_ln:
             o = G.linear_any(actx, o_w, o_b)
             z1, f_in, m2, r2 = Fx.ln_fwd(o, x2d, g2, b2, eps, p_h, rng, s1)

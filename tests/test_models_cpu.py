@@ -86,6 +86,61 @@ def test_ln_bwd_from_output_matches_stored_z_form():
         Fx.ln_bwd(dout, None, None, m, rs, gamma, 0.1, rng, 7)
 
 
+@pytest.mark.parametrize("ratio,bound", [(8.0, (3e-3, 2e-2)), (64.0, None)])
+def test_ln_memeff_error_at_the_guard_limit(ratio, bound):
+    """x-hat = (out - beta) / gamma from a bf16 output: the error grows with |beta| / |gamma|.  At
+    the guard's limit (ratio 8, models/transformer.py _LN_BETA_RATIO) dx and dgamma stay within
+    0.3 % / 2 % of the fp32 stored-z backward; at ratio 64 -- what the guard refuses -- dgamma is
+    off by ~10 %."""
+    from distributed_training_and_deepspeed_amd.models import transformer as TR
+    from distributed_training_and_deepspeed_amd.ops import functional as Fx
+    from distributed_training_and_deepspeed_amd.ops.rng import RngState
+    torch.manual_seed(0)
+    rows, h = 512, 256
+    y, r, dout = (torch.randn(rows, h) for _ in range(3))
+    beta = torch.empty(h).uniform_(-1, 1)
+    gamma = torch.clamp(beta.abs() / ratio, min=1e-3) * torch.sign(torch.randn(h))
+    rng = RngState(3)
+    res = {}
+    for fo in (False, True):
+        z, o, m, rs = Fx.ln_fwd(y, r, gamma, beta, 1e-5, 0.0, rng, 7, store_z=not fo)
+        dg, db = torch.zeros(h), torch.zeros(h)
+        kw = dict(xout=o.bfloat16().float(), beta=beta) if fo else {}
+        dz, _ = Fx.ln_bwd(dout, None, z, m, rs, gamma, 0.0, rng, 7, want_dz=True, want_dy=False, dgamma=dg,
+                          dbeta=db, **kw)
+        res[fo] = (dz, dg)
+    err = [((a - b).norm() / b.norm()).item() for a, b in zip(res[True], res[False])]
+    if bound is None:
+        assert err[1] > 0.05
+        assert ratio > TR._LN_BETA_RATIO
+    else:
+        assert ratio <= TR._LN_BETA_RATIO and err[0] < bound[0] and err[1] < bound[1], err
+
+
+def test_loading_ill_conditioned_layernorm_selects_stored_z_backward():
+    """A state dict whose post-LN gamma is (near) zero where beta is not switches that model to the
+    stored-z LayerNorm backward at load time; a well-conditioned one (or an explicit choice) does
+    not."""
+    from distributed_training_and_deepspeed_amd.models import build_model
+    from distributed_training_and_deepspeed_amd.models import transformer as TR
+    m = build_model("tiny")
+    assert m.rt.ln_memeff is None and TR.ln_memeff_safe(m.layers)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    assert m.rt.ln_memeff is None
+    key = [k for k in sd if k.endswith("ln2_g")][1]
+    sd[key][5] = 0.0
+    sd[key.replace("ln2_g", "ln2_b")][5] = 0.5
+    m2 = build_model("tiny")
+    with pytest.warns(RuntimeWarning, match="stored-z"):
+        m2.load_state_dict(sd)
+    assert m2.rt.ln_memeff is False and not TR.ln_memeff_safe(m2.layers)
+    m3 = build_model("tiny")
+    m3.rt.ln_memeff = True
+    m3.load_state_dict(sd)
+    assert m3.rt.ln_memeff is True
+
+
 def test_mlm_masking_law():
     cfg = C.BERT_BASE
     ds = SyntheticLMDataset(cfg, 64, seq_len=512, seed=0)
