@@ -76,6 +76,10 @@ def parse():
     ap.add_argument("--force-collectives", action="store_true",
                     help="issue the DDP bucket all-reduces / ZeRO reduce-scatters and all-gathers through RCCL "
                          "even at world size 1 (the N > 1 data path on one GPU)")
+    ap.add_argument("--comm-init", action="store_true",
+                    help="diagnostic: initialise the RCCL process group even when no collective runs")
+    ap.add_argument("--ddp-overlap", default="on", choices=["on", "off"],
+                    help="diagnostic: off launches every bucket collective after the backward")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
     return ap.parse_args()
@@ -103,7 +107,7 @@ def main():
             from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
             tuned = use_tuned_gemms()
     device = torch.device("cuda", local) if cuda else torch.device("cpu")
-    if world > 1 or args.zero_stage is not None or args.force_collectives:   # ZeRO always runs on a group
+    if world > 1 or args.zero_stage is not None or args.force_collectives or args.comm_init:   # ZeRO: always a group
         comm.init(rank=rank, world_size=world, local_rank=local)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     cfg = get_config(args.model)
@@ -132,7 +136,8 @@ def main():
         ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, grad_dtype=gdt,
                                       small_bucket_allreduce=args.small_bucket_allreduce,
                                       async_wgrad=args.async_wgrad == "on",
-                                      force_collectives=args.force_collectives)
+                                      force_collectives=args.force_collectives,
+                                      overlap=args.ddp_overlap == "on")
         opt = hf_adamw(ddp.parameters(), lr=5e-5)
 
     B, S = args.batch_size, args.seq_len
@@ -247,7 +252,7 @@ def main():
             "loss_last": round(float(loss.detach()), 4),
         }
         print(json.dumps(res), flush=True)
-    if world > 1 or zero or args.force_collectives:
+    if world > 1 or zero or args.force_collectives or args.comm_init:
         comm.destroy()
 
 
