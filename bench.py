@@ -76,8 +76,10 @@ def parse():
     ap.add_argument("--force-collectives", action="store_true",
                     help="issue the DDP bucket all-reduces / ZeRO reduce-scatters and all-gathers through RCCL "
                          "even at world size 1 (the N > 1 data path on one GPU)")
-    ap.add_argument("--comm-init", action="store_true",
-                    help="diagnostic: initialise the RCCL process group even when no collective runs")
+    ap.add_argument("--comm-init", default="none", choices=["none", "rccl", "rccl-lazy", "rccl-destroy", "gloo"],
+                    help="diagnostic: initialise a process group even when no collective runs (rccl: "
+                         "comm.init; rccl-lazy: no device_id, so no communicator is created; "
+                         "rccl-destroy: comm.init then destroy before the model is built; gloo)")
     ap.add_argument("--ddp-overlap", default="on", choices=["on", "off"],
                     help="diagnostic: off launches every bucket collective after the backward")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -107,8 +109,18 @@ def main():
             from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
             tuned = use_tuned_gemms()
     device = torch.device("cuda", local) if cuda else torch.device("cpu")
-    if world > 1 or args.zero_stage is not None or args.force_collectives or args.comm_init:   # ZeRO: always a group
+    if world > 1 or args.zero_stage is not None or args.force_collectives:   # ZeRO always runs on a group
         comm.init(rank=rank, world_size=world, local_rank=local)
+    elif args.comm_init != "none":
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        if args.comm_init in ("rccl", "rccl-destroy"):
+            comm.init(rank=rank, world_size=world, local_rank=local)
+            if args.comm_init == "rccl-destroy":
+                comm.destroy()
+        else:
+            dist.init_process_group(backend="nccl" if args.comm_init == "rccl-lazy" else "gloo", rank=rank,
+                                    world_size=world)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     cfg = get_config(args.model)
     mlm = cfg.family == "bert"
@@ -252,7 +264,7 @@ def main():
             "loss_last": round(float(loss.detach()), 4),
         }
         print(json.dumps(res), flush=True)
-    if world > 1 or zero or args.force_collectives or args.comm_init:
+    if world > 1 or zero or args.force_collectives or dist.is_initialized():
         comm.destroy()
 
 
