@@ -76,10 +76,12 @@ def parse():
     ap.add_argument("--force-collectives", action="store_true",
                     help="issue the DDP bucket all-reduces / ZeRO reduce-scatters and all-gathers through RCCL "
                          "even at world size 1 (the N > 1 data path on one GPU)")
-    ap.add_argument("--comm-init", default="none", choices=["none", "rccl", "rccl-lazy", "rccl-destroy", "gloo"],
+    ap.add_argument("--comm-init", default="none", choices=["none", "rccl", "rccl-lazy", "rccl-destroy", "gloo", "uncached", "finegrained", "hostmem"],
                     help="diagnostic: initialise a process group even when no collective runs (rccl: "
                          "comm.init; rccl-lazy: no device_id, so no communicator is created; "
-                         "rccl-destroy: comm.init then destroy before the model is built; gloo)")
+                         "rccl-destroy: comm.init then destroy before the model is built; gloo; "
+                         "uncached / finegrained / hostmem: only the 512 MB uncached, fine-grained "
+                         "device or 4 MB pinned host buffer RCCL's init allocates)")
     ap.add_argument("--ddp-overlap", default="on", choices=["on", "off"],
                     help="diagnostic: off launches every bucket collective after the backward")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -114,7 +116,19 @@ def main():
     elif args.comm_init != "none":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29561")
-        if args.comm_init in ("rccl", "rccl-destroy"):
+        if args.comm_init in ("uncached", "finegrained", "hostmem"):
+            import ctypes
+            # the HIP runtime torch already loaded (a second copy would be a second runtime)
+            hip = ctypes.CDLL(next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln))
+            buf = ctypes.c_void_p()
+            if args.comm_init == "hostmem":
+                rc = hip.hipHostMalloc(ctypes.byref(buf), ctypes.c_size_t(4 << 20), ctypes.c_uint(0))
+            else:
+                rc = hip.hipExtMallocWithFlags(ctypes.byref(buf), ctypes.c_size_t(512 << 20),
+                                               ctypes.c_uint(3 if args.comm_init == "uncached" else 1))
+            if rc != 0:
+                raise RuntimeError(f"diagnostic allocation failed: hip error {rc}")
+        elif args.comm_init in ("rccl", "rccl-destroy"):
             comm.init(rank=rank, world_size=world, local_rank=local)
             if args.comm_init == "rccl-destroy":
                 comm.destroy()
