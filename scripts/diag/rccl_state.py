@@ -19,10 +19,12 @@ def state():
     for name, lim in (("stack", 0), ("printf_fifo", 1), ("malloc_heap", 2)):
         v = ctypes.c_size_t()
         out[name] = (hip.hipDeviceGetLimit(ctypes.byref(v), ctypes.c_int(lim)), v.value)
+        hip.hipGetLastError()   # an unsupported limit latches an error torch would raise later
     f = ctypes.c_uint()
     out["device_flags"] = (hip.hipGetDeviceFlags(ctypes.byref(f)), f.value)
     c = ctypes.c_int()
     out["cache_config"] = (hip.hipDeviceGetCacheConfig(ctypes.byref(c)), c.value)
+    hip.hipGetLastError()
     out["env_changed"] = None
     return out
 
