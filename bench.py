@@ -76,10 +76,13 @@ def parse():
     ap.add_argument("--force-collectives", action="store_true",
                     help="issue the DDP bucket all-reduces / ZeRO reduce-scatters and all-gathers through RCCL "
                          "even at world size 1 (the N > 1 data path on one GPU)")
-    ap.add_argument("--comm-init", default="none", choices=["none", "rccl", "rccl-lazy", "rccl-destroy", "gloo", "uncached", "finegrained", "hostmem"],
+    ap.add_argument("--comm-init", default="none", choices=["none", "rccl", "rccl-lazy", "rccl-destroy", "rccl-late", "rccl-after-warmup", "gloo", "uncached",
+                             "finegrained", "hostmem"],
                     help="diagnostic: initialise a process group even when no collective runs (rccl: "
                          "comm.init; rccl-lazy: no device_id, so no communicator is created; "
-                         "rccl-destroy: comm.init then destroy before the model is built; gloo; "
+                         "rccl-destroy: comm.init then destroy before the model is built; rccl-late / "
+                         "rccl-after-warmup: comm.init after the model and data are allocated / after "
+                         "the warm-up steps; gloo; "
                          "uncached / finegrained / hostmem: only the 512 MB uncached, fine-grained "
                          "device or 4 MB pinned host buffer RCCL's init allocates)")
     ap.add_argument("--ddp-overlap", default="on", choices=["on", "off"],
@@ -128,6 +131,8 @@ def main():
                                                ctypes.c_uint(3 if args.comm_init == "uncached" else 1))
             if rc != 0:
                 raise RuntimeError(f"diagnostic allocation failed: hip error {rc}")
+        elif args.comm_init in ("rccl-late", "rccl-after-warmup"):
+            pass   # below
         elif args.comm_init in ("rccl", "rccl-destroy"):
             comm.init(rank=rank, world_size=world, local_rank=local)
             if args.comm_init == "rccl-destroy":
@@ -214,9 +219,13 @@ def main():
         if world > 1:
             dist.barrier()
 
+    if args.comm_init == "rccl-late":
+        comm.init(rank=rank, world_size=world, local_rank=local)
     for i in range(args.warmup):
         loss = step(i)
     sync()
+    if args.comm_init == "rccl-after-warmup":
+        comm.init(rank=rank, world_size=world, local_rank=local)
     first_loss = float(loss.detach()) if args.warmup else float("nan")
     sync()
     t0 = time.perf_counter()
