@@ -87,6 +87,9 @@ def parse():
                          "device or 4 MB pinned host buffer RCCL's init allocates)")
     ap.add_argument("--ddp-overlap", default="on", choices=["on", "off"],
                     help="diagnostic: off launches every bucket collective after the backward")
+    ap.add_argument("--prewarm", default="none", choices=["none", "tiny", "full"],
+                    help="diagnostic: one forward+backward of the model (tiny: batch 1; full: the bench "
+                         "batch) before the process group is created")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
     return ap.parse_args()
@@ -114,6 +117,16 @@ def main():
             from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
             tuned = use_tuned_gemms()
     device = torch.device("cuda", local) if cuda else torch.device("cpu")
+    if args.prewarm != "none":
+        _m = build_model(args.model, impl=args.impl, dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32,
+                         device=device, seed=1)
+        _m.train()
+        _b = 1 if args.prewarm == "tiny" else args.batch_size
+        _ds = SyntheticLMDataset(get_config(args.model), num_samples=_b, seq_len=args.seq_len, seed=7)
+        _m(_ds.input_ids.to(device), labels=_ds.labels.to(device)).loss.backward()
+        if cuda:
+            torch.cuda.synchronize()
+        del _m, _ds
     if world > 1 or args.zero_stage is not None or args.force_collectives:   # ZeRO always runs on a group
         comm.init(rank=rank, world_size=world, local_rank=local)
     elif args.comm_init != "none":
