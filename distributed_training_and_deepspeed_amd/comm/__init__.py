@@ -40,6 +40,37 @@ def default_backend() -> str:
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 
+def prewarm_device_code(device, level: str | None = None) -> None:
+    """Load this process's GPU code objects BEFORE the RCCL communicator is created.
+
+    Measured on MI355X (docs/PERFORMANCE.md, "Kernels loaded after the RCCL communicator"): every
+    kernel whose code object is first loaded after ``ncclCommInitRank`` runs 5-25 % longer for
+    the whole life of the process -- same L2 / HBM traffic, more cycles (profiles/r4_s40_*) --
+    while kernels loaded before it keep their speed (profiles/r4_s41_*, r4_s42_*, r4_s43_*).
+    The BERT-base step lost ~10 % to it at every world size that creates a communicator.  So
+    before the group exists, launch one kernel of the framework's HIP module (_dtd_kernels.so),
+    a torch elementwise kernel and hipBLASLt GEMMs of the bf16 / fp32 layouts and bias forms the
+    training step uses.  ``level`` (env ``DTD_COMM_PREWARM``): "full" (default), "torch" (the
+    torch kernel only; diagnostic) or "0" (off)."""
+    level = level or os.environ.get("DTD_COMM_PREWARM", "full")
+    if level == "0" or not torch.cuda.is_available():
+        return
+    dev = torch.device(device)
+    x = torch.ones(256, 256, device=dev)
+    if level != "torch":
+        from ..ops import functional as Fx
+        Fx.act_fwd(x.to(torch.bfloat16), "gelu")
+        for dt in (torch.bfloat16, torch.float32):
+            a = torch.randn(512, 768, device=dev, dtype=dt)
+            w = torch.randn(768, 768, device=dev, dtype=dt)
+            b = torch.zeros(768, device=dev, dtype=dt)
+            torch.nn.functional.linear(a, w, b)
+            torch.nn.functional.linear(a, w)
+            a.t() @ a
+            a @ w
+    torch.cuda.synchronize(dev)
+
+
 def init(rank: int | None = None, world_size: int | None = None, backend: str | None = None,
          master_addr: str | None = None, master_port: int | str | None = None, local_rank: int | None = None,
          timeout_s: float = 1800.0, init_method: str | None = None,
@@ -68,6 +99,7 @@ def init(rank: int | None = None, world_size: int | None = None, backend: str | 
     kw = {}
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
+        prewarm_device_code(torch.device("cuda", local_rank))
         kw["device_id"] = torch.device("cuda", local_rank)
         if high_priority is None:
             high_priority = os.environ.get("DTD_RCCL_HIGH_PRIORITY", "1") == "1"
