@@ -50,12 +50,19 @@ def prewarm_device_code(device, level: str | None = None) -> None:
     The BERT-base step lost ~10 % to it at every world size that creates a communicator.  So
     before the group exists, launch one kernel of the framework's HIP module (_dtd_kernels.so),
     a torch elementwise kernel and hipBLASLt GEMMs of the bf16 / fp32 layouts and bias forms the
-    training step uses.  ``level`` (env ``DTD_COMM_PREWARM``): "full" (default), "torch" (the
-    torch kernel only; diagnostic) or "0" (off)."""
+    training step uses, and create torch's side-stream pools.  ``level`` (env ``DTD_COMM_PREWARM``):
+    "full" (default), "streams" (stream pools only), "kernels" (code objects only), "torch" (one
+    torch kernel; diagnostic) or "0" (off)."""
     level = level or os.environ.get("DTD_COMM_PREWARM", "full")
     if level == "0" or not torch.cuda.is_available():
         return
     dev = torch.device(device)
+    if level in ("full", "streams"):
+        # torch's side-stream pools (every torch.cuda.Stream() of the framework comes from them)
+        torch.cuda.Stream(dev)
+        torch.cuda.Stream(dev, priority=-1)
+        if level == "streams":
+            return
     x = torch.ones(256, 256, device=dev)
     if level != "torch":
         from ..ops import functional as Fx
