@@ -87,9 +87,10 @@ def parse():
                          "device or 4 MB pinned host buffer RCCL's init allocates)")
     ap.add_argument("--ddp-overlap", default="on", choices=["on", "off"],
                     help="diagnostic: off launches every bucket collective after the backward")
-    ap.add_argument("--prewarm", default="none", choices=["none", "tiny", "full"],
-                    help="diagnostic: one forward+backward of the model (tiny: batch 1; full: the bench "
-                         "batch) before the process group is created")
+    ap.add_argument("--prewarm", default="auto", choices=["auto", "none", "layer1", "tiny", "full"],
+                    help="one forward+backward of a throwaway copy of the model before the RCCL group is "
+                         "created (auto: a 1-layer copy at batch 1 whenever a group is created; tiny: "
+                         "full depth, batch 1; full: full depth at the bench batch; utils/prewarm.py)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
     return ap.parse_args()
@@ -108,6 +109,7 @@ def main():
     from distributed_training_and_deepspeed_amd.models import build_model, get_config
     from distributed_training_and_deepspeed_amd.optim import hf_adamw
     from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
+    from distributed_training_and_deepspeed_amd.utils.prewarm import prewarm_enabled, prewarm_model_kernels
 
     cuda = torch.cuda.is_available()
     tuned = False
@@ -117,16 +119,16 @@ def main():
             from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
             tuned = use_tuned_gemms()
     device = torch.device("cuda", local) if cuda else torch.device("cpu")
-    if args.prewarm != "none":
-        _m = build_model(args.model, impl=args.impl, dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32,
-                         device=device, seed=1)
-        _m.train()
-        _b = 1 if args.prewarm == "tiny" else args.batch_size
-        _ds = SyntheticLMDataset(get_config(args.model), num_samples=_b, seq_len=args.seq_len, seed=7)
-        _m(_ds.input_ids.to(device), labels=_ds.labels.to(device)).loss.backward()
-        if cuda:
-            torch.cuda.synchronize()
-        del _m, _ds
+    group = world > 1 or args.zero_stage is not None or args.force_collectives or args.comm_init != "none"
+    if cuda and args.prewarm != "none" and (args.prewarm != "auto" or (group and prewarm_enabled())):
+        # the step's kernels run once before the RCCL communicator exists (utils/prewarm.py:
+        # kernels first launched after it run 5-25 % slower for the life of the process)
+        prewarm_model_kernels(args.model, device, dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32,
+                              impl=args.impl, seq_len=args.seq_len,
+                              layers=None if args.prewarm in ("tiny", "full") else 1,
+                              batch=args.batch_size if args.prewarm == "full" else 1,
+                              static_mlm=not args.dense_mlm_head and args.mlm_capacity == "static",
+                              **({"sparse_mlm_head": not args.dense_mlm_head} if get_config(args.model).family == "bert" else {}))
     if world > 1 or args.zero_stage is not None or args.force_collectives:   # ZeRO always runs on a group
         comm.init(rank=rank, world_size=world, local_rank=local)
     elif args.comm_init != "none":

@@ -1,0 +1,56 @@
+"""Launch the training step's kernels once BEFORE the RCCL communicator is created.
+
+Measured on MI355X (docs/PERFORMANCE.md, "Kernels first launched after the RCCL communicator"):
+after ``ncclCommInitRank`` every kernel of the BERT step that had not been launched yet runs
+5-25 % longer for the rest of the process -- identical L2 / HBM traffic, more cycles
+(profiles/r4_s40_rccl_init_pmc.jsonl) -- and the N > 1 step loses ~10 %
+(profiles/r4_s33_*, r4_s43_*).  Kernels launched before it keep their speed: creating the group
+after the warm-up steps, or after one batch-1 forward/backward of the model, costs nothing.
+Loading the code objects, torch's stream pools or a few GEMMs first does not help
+(profiles/r4_s44_*, r4_s45_*): the step's own kernels have to run once.
+
+``prewarm_model_kernels`` builds a throwaway copy of the model (``layers`` deep -- every encoder
+layer runs the same kernels), runs one batch-1 forward + backward on synthetic tokens and frees
+it.  The entry scripts call it before ``comm.init`` (env ``DTD_PREWARM=0`` turns it off)."""
+from __future__ import annotations
+
+import dataclasses
+import os
+
+import torch
+
+
+def prewarm_enabled() -> bool:
+    return os.environ.get("DTD_PREWARM", "1") != "0" and torch.cuda.is_available()
+
+
+def prewarm_model_kernels(name: str, device, dtype=torch.bfloat16, impl: str = "auto", seq_len: int = 512,
+                          layers: int | None = 1, batch: int = 1, static_mlm: bool = True,
+                          **model_kw) -> None:
+    from ..data import SyntheticLMDataset
+    from ..models import get_config
+    from ..models.bert import BertForMaskedLM
+    from ..models.causal_lm import CausalLM
+    from ..models.transformer import Runtime
+    from ..ops.rng import RngState
+    dev = torch.device(device)
+    cfg = get_config(name)
+    if layers is not None:
+        cfg = dataclasses.replace(cfg, num_layers=min(layers, cfg.num_layers))
+    rng_state = torch.random.get_rng_state()
+    rt = Runtime(impl=impl, rng=RngState(seed=0, device=dev))
+    cls = BertForMaskedLM if cfg.family == "bert" else CausalLM
+    model = cls(cfg, rt=rt, **model_kw).to(device=dev, dtype=dtype)
+    model.train()
+    if cfg.family == "bert" and static_mlm:
+        from .graphs import mlm_capacity
+        rt.mlm_capacity = -(-mlm_capacity(batch * seq_len) // 256) * 256
+        rt.mlm_overflow = torch.zeros((), dtype=torch.bool, device=dev)
+    ds = SyntheticLMDataset(cfg, num_samples=batch, seq_len=min(seq_len, cfg.max_positions), mlm=cfg.family == "bert",
+                            seed=0)
+    out = model(ds.input_ids.to(dev), labels=ds.labels.to(dev))
+    out.loss.backward()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    del model, out
+    torch.random.set_rng_state(rng_state)
