@@ -39,11 +39,20 @@ from distributed_training_and_deepspeed_amd.optim import hf_adamw  # noqa: E402
 from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel  # noqa: E402
 from distributed_training_and_deepspeed_amd.utils import get_device_count  # noqa: E402
 from distributed_training_and_deepspeed_amd.utils.checkpoint import load_checkpoint, save_checkpoint  # noqa: E402
+from distributed_training_and_deepspeed_amd.utils.prewarm import prewarm_enabled, prewarm_model_kernels  # noqa: E402
 from distributed_training_and_deepspeed_amd.utils.tracing import StepTimer, enable_markers, marker  # noqa: E402
 
 
 def train(rank, world_size, batch_size, training_steps, bucket_size, model_name, opts):
     backend = opts.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+    if backend == "nccl" and prewarm_enabled():
+        # the step's kernels run once before the RCCL communicator exists: kernels first launched
+        # after it run 5-25 % slower for the life of the process (utils/prewarm.py)
+        local = rank % max(1, get_device_count())
+        torch.cuda.set_device(local)
+        prewarm_model_kernels({"base": "bert-base-cased", "large": "bert-large-cased"}.get(model_name, model_name),
+                              torch.device("cuda", local), dtype={"bf16": torch.bfloat16, "fp32": torch.float32}[opts.dtype],
+                              impl=opts.impl, seq_len=opts.seq_len)
     comm.init(rank=rank, world_size=world_size, backend=backend, local_rank=rank % max(1, get_device_count()))
     cuda = backend == "nccl"
     device = torch.device("cuda", torch.cuda.current_device()) if cuda else torch.device("cpu")

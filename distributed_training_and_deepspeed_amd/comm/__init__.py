@@ -40,44 +40,6 @@ def default_backend() -> str:
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 
-def prewarm_device_code(device, level: str | None = None) -> None:
-    """Load this process's GPU code objects BEFORE the RCCL communicator is created.
-
-    Measured on MI355X (docs/PERFORMANCE.md, "Kernels loaded after the RCCL communicator"): every
-    kernel whose code object is first loaded after ``ncclCommInitRank`` runs 5-25 % longer for
-    the whole life of the process -- same L2 / HBM traffic, more cycles (profiles/r4_s40_*) --
-    while kernels loaded before it keep their speed (profiles/r4_s41_*, r4_s42_*, r4_s43_*).
-    The BERT-base step lost ~10 % to it at every world size that creates a communicator.  So
-    before the group exists, launch one kernel of the framework's HIP module (_dtd_kernels.so),
-    a torch elementwise kernel and hipBLASLt GEMMs of the bf16 / fp32 layouts and bias forms the
-    training step uses, and create torch's side-stream pools.  ``level`` (env ``DTD_COMM_PREWARM``):
-    "full" (default), "streams" (stream pools only), "kernels" (code objects only), "torch" (one
-    torch kernel; diagnostic) or "0" (off)."""
-    level = level or os.environ.get("DTD_COMM_PREWARM", "full")
-    if level == "0" or not torch.cuda.is_available():
-        return
-    dev = torch.device(device)
-    if level in ("full", "streams"):
-        # torch's side-stream pools (every torch.cuda.Stream() of the framework comes from them)
-        torch.cuda.Stream(dev)
-        torch.cuda.Stream(dev, priority=-1)
-        if level == "streams":
-            return
-    x = torch.ones(256, 256, device=dev)
-    if level != "torch":
-        from ..ops import functional as Fx
-        Fx.act_fwd(x.to(torch.bfloat16), "gelu")
-        for dt in (torch.bfloat16, torch.float32):
-            a = torch.randn(512, 768, device=dev, dtype=dt)
-            w = torch.randn(768, 768, device=dev, dtype=dt)
-            b = torch.zeros(768, device=dev, dtype=dt)
-            torch.nn.functional.linear(a, w, b)
-            torch.nn.functional.linear(a, w)
-            a.t() @ a
-            a @ w
-    torch.cuda.synchronize(dev)
-
-
 def init(rank: int | None = None, world_size: int | None = None, backend: str | None = None,
          master_addr: str | None = None, master_port: int | str | None = None, local_rank: int | None = None,
          timeout_s: float = 1800.0, init_method: str | None = None,
@@ -90,7 +52,11 @@ def init(rank: int | None = None, world_size: int | None = None, backend: str | 
     created with high priority, so the dispatcher hands freed CUs to the all-reduce /
     reduce-scatter kernels that DDP and ZeRO launch during backward before the next compute
     workgroups -- the collectives overlap the backward instead of queueing behind it.  The
-    persistent GEMMs tolerate the CUs they lose (dynamic tile queue, ops/gemm.py)."""
+    persistent GEMMs tolerate the CUs they lose (dynamic tile queue, ops/gemm.py).
+
+    Kernels first launched after the communicator exists run 5-25 % slower for the rest of the
+    process: run the step's kernels once before calling this (utils/prewarm.py; the entry
+    scripts do)."""
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     rank = env_rank() if rank is None else rank
@@ -106,7 +72,6 @@ def init(rank: int | None = None, world_size: int | None = None, backend: str | 
     kw = {}
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
-        prewarm_device_code(torch.device("cuda", local_rank))
         kw["device_id"] = torch.device("cuda", local_rank)
         if high_priority is None:
             high_priority = os.environ.get("DTD_RCCL_HIGH_PRIORITY", "1") == "1"

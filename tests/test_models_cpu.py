@@ -310,3 +310,14 @@ def test_attention_keep_word_layout_roundtrip():
     enc = torch.where(enc >= 2**31, enc - 2**32, enc).to(torch.int32)
     a, b = A.decode_masks(enc, B, H, S)
     assert torch.equal(a, keep) and torch.equal(b, keep)
+
+
+@pytest.mark.parametrize("name", ["tiny", "causal-tiny"])
+def test_prewarm_model_kernels_leaves_the_global_rng_alone(name):
+    """utils/prewarm.py: the throwaway 1-layer forward/backward that the entry scripts run before
+    creating the RCCL group must not shift the global torch RNG (the real model's init draws)."""
+    from distributed_training_and_deepspeed_amd.utils.prewarm import prewarm_model_kernels
+    torch.manual_seed(11)
+    state = torch.random.get_rng_state()
+    prewarm_model_kernels(name, "cpu", dtype=torch.float32, seq_len=64)
+    assert torch.equal(state, torch.random.get_rng_state())

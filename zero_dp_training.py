@@ -43,12 +43,20 @@ from distributed_training_and_deepspeed_amd.launch import launch  # noqa: E402
 from distributed_training_and_deepspeed_amd.models import build_model, get_config  # noqa: E402
 from distributed_training_and_deepspeed_amd.parallel.zero import initialize  # noqa: E402
 from distributed_training_and_deepspeed_amd.profiling import memory_status  # noqa: E402
+from distributed_training_and_deepspeed_amd.utils.prewarm import prewarm_enabled, prewarm_model_kernels  # noqa: E402
 
 
 def train(model_name, batch_size, training_steps, stage, opts):
     rank = int(os.getenv("LOCAL_RANK", "0"))
     world_size = int(os.getenv("WORLD_SIZE", "1"))
     backend = opts.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+    if backend == "nccl" and prewarm_enabled():
+        # the step's kernels run once before the RCCL communicator exists: kernels first launched
+        # after it run 5-25 % slower for the life of the process (utils/prewarm.py)
+        torch.cuda.set_device(rank)
+        prewarm_model_kernels(model_name, torch.device("cuda", rank),
+                              dtype={"bf16": torch.bfloat16, "fp32": torch.float32}[opts.dtype], impl=opts.impl,
+                              seq_len=opts.seq_len, static_mlm=False)
     comm.init(backend=backend)
     cuda = backend == "nccl"
     device = torch.device("cuda", rank) if cuda else torch.device("cpu")
