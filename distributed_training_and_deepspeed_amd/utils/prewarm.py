@@ -11,7 +11,7 @@ Loading the code objects, torch's stream pools or a few GEMMs first does not hel
 
 ``prewarm_model_kernels`` builds a throwaway copy of the model (``layers`` deep -- every encoder
 layer runs the same kernels), runs one batch-1 forward + backward on synthetic tokens and frees
-it.  The entry scripts call it before ``comm.init`` (env ``DTD_PREWARM=0`` turns it off)."""
+it (and one fused Adam step on its gradients).  The entry scripts call it before ``comm.init`` (env ``DTD_PREWARM=0`` turns it off)."""
 from __future__ import annotations
 
 import dataclasses
@@ -25,7 +25,7 @@ def prewarm_enabled() -> bool:
 
 
 def prewarm_model_kernels(name: str, device, dtype=torch.bfloat16, impl: str = "auto", seq_len: int = 512,
-                          layers: int | None = 1, batch: int = 1, static_mlm: bool = True,
+                          layers: int | None = 1, batch: int = 1, static_mlm: bool = True, optimizer: bool = True,
                           **model_kw) -> None:
     from ..data import SyntheticLMDataset
     from ..models import get_config
@@ -50,6 +50,12 @@ def prewarm_model_kernels(name: str, device, dtype=torch.bfloat16, impl: str = "
                             seed=0)
     out = model(ds.input_ids.to(dev), labels=ds.labels.to(dev))
     out.loss.backward()
+    if optimizer:
+        # the fused Adam kernel (DDP's hf_adamw and the ZeRO engine's optimizer) runs once too
+        from ..optim import hf_adamw
+        opt = hf_adamw([p for p in model.parameters() if p.grad is not None], lr=0.0)
+        opt.step()
+        del opt
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     del model, out
