@@ -59,4 +59,6 @@ def prewarm_model_kernels(name: str, device, dtype=torch.bfloat16, impl: str = "
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     del model, out
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()   # hand the throwaway model's memory back (large ZeRO-3 runs)
     torch.random.set_rng_state(rng_state)
