@@ -30,11 +30,10 @@ import os
 
 # HIP hardware queues per process: the box default (4) is fewer than the streams of the N > 1
 # step (compute, keep-mask, optimizer, finalize and RCCL's own); streams sharing a queue
-# serialise their cross-stream waits.  Raised to 8 before anything initialises HIP
+# serialise their cross-stream waits.  Set to 8 (when unset) before anything initialises HIP
 # (docs/PERFORMANCE.md, "Hardware queues").
-_HWQ = os.environ.get("GPU_MAX_HW_QUEUES", "")
-if not _HWQ.isdigit() or int(_HWQ) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# A value the user set is kept as it is (e.g. 4 for an A/B run); the value in effect is logged.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 import sys
 import time
 
@@ -273,8 +272,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": ("synthetic (random token ids, HF MLM 15%/80/10/10 masking; random-init weights)" if mlm
-                     else "synthetic (random token ids, causal labels = input_ids; random-init weights)"),
+            "data": ("synthetic (random token ids, HF MLM 15%/80/10/10 masking; random-init weights; "
+                     "batches pre-staged on device)" if mlm
+                     else "synthetic (random token ids, causal labels = input_ids; random-init weights; "
+                          "batches pre-staged on device)"),
             "config": {
                 "model": cfg.name,
                 "params": sum(p.numel() for p in model.parameters()),
@@ -297,6 +298,7 @@ def main():
                 "async_wgrad": args.async_wgrad == "on",
                 "opt_overlap": opt_overlap,
                 "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if cuda else None,
+                "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             },
             "loss_first": round(first_loss, 4),
             "loss_last": round(float(loss.detach()), 4),

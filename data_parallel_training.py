@@ -19,11 +19,10 @@ import os
 
 # HIP hardware queues per process: the box default (4) is fewer than the streams of the N > 1
 # step (compute, keep-mask, optimizer, finalize and RCCL's own); streams sharing a queue
-# serialise their cross-stream waits.  Raised to 8 before anything initialises HIP
+# serialise their cross-stream waits.  Set to 8 (when unset) before anything initialises HIP
 # (docs/PERFORMANCE.md, "Hardware queues").
-_HWQ = os.environ.get("GPU_MAX_HW_QUEUES", "")
-if not _HWQ.isdigit() or int(_HWQ) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# A value the user set is kept as it is (e.g. 4 for an A/B run); the value in effect is logged.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 import sys
 import time
 
@@ -97,9 +96,11 @@ def train(rank, world_size, batch_size, training_steps, bucket_size, model_name,
 
     graphed, batches, warm, loss = None, iter(loader), [], None
     if opts.graph == "auto":
-        # small per-GPU batches are host-launch bound: replay the whole step -- bucket all-reduces
-        # included (RCCL collectives inside the capture: tests/test_graph_gpu.py, force_collectives)
-        opts.graph = "on" if (cuda and batch_size <= 32 and not opts.markers) else "off"
+        # small per-GPU batches are host-launch bound: replay the whole step.  Only at world 1 by
+        # default: a captured step with the bucket all-reduces inside it has been checked against
+        # eager on one rank (tests/test_graph_gpu.py, force_collectives) but not yet replayed in
+        # lockstep across ranks on a multi-GPU node; `--graph on` opts in at world > 1.
+        opts.graph = "on" if (cuda and world_size == 1 and batch_size <= 32 and not opts.markers) else "off"
     if opts.graph == "on" and cuda:
         # whole step (forward, backward + bucket all-reduces, optimizer, RNG advance) replayed as
         # one hipGraph: the reference's 4 x 512-token batches are host-launch bound otherwise

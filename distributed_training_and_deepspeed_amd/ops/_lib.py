@@ -84,6 +84,10 @@ _SIGS = {
     "dtd_gemm_tn_supported": (I, [I, I, I]),
     "dtd_gemm_tn_splits": (I, [I, I, I]),
     "dtd_gemm_tn": (I, [P, I, P, I, P, I, I, I, I, P]),
+    # wgrad.hip
+    "dtd_wgrad_tn_supported": (I, [I, I, I]),
+    "dtd_wgrad_tn_splits": (I, [I, I, I]),
+    "dtd_wgrad_tn": (I, [I, P, I, P, I, P, I, I, I, I, P]),
     # gemm4.hip
     "dtd_gemm4_supported": (I, [I, I, I]),
     "dtd_gemm4_bt": (I, [I, P, I, P, I, P, I, P, I, I, I, P]),

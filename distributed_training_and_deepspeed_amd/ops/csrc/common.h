@@ -244,6 +244,31 @@ __host__ __device__ __forceinline__ uint32_t keep_threshold(float p) {
   return t >= 65536.0f ? 65536u : (uint32_t)(t + 0.5f);
 }
 
+// One LDS-DMA piece (buffer_load_dwordx4 ... lds: 16 bytes per lane to LDS address lds + 16 lane)
+// as inline asm.  Issued through the builtin, hipcc's wait-count pass treats every later LDS read
+// (and the next LDS-DMA) as a possible alias of the in-flight DMA and drains the whole vector-memory
+// queue before it (s_waitcnt vmcnt(0)): the counted waits of a multi-stage LDS ring are then dead
+// letters and every stage lands before the next is issued.  Hidden in asm the DMA is counted only by
+// the kernel's own s_waitcnt vmcnt(N) (a compiler-visible load or store in between only makes those
+// waits stricter: the counter retires in issue order).  M0 is set inside the statement (the
+// compiler does not preserve it around asm) and restored after it; the s_nop covers the
+// M0-write -> LDS-DMA hazard.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
+  // the LDS base and scalar offset must be wave-uniform (SGPR operands): readfirstlane makes that
+  // provable where the caller's expression is not (a no-op on values already in SGPRs)
+  const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds);
+  soff = __builtin_amdgcn_readfirstlane(soff);
+#ifdef DTD_DMA_BUILTIN   // A/B builds only: the builtin form (hipcc's drains included)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(uintptr_t)m, 16, voff, soff,
+                                           0, 0);
+  return;
+#endif
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "s"(m), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+
 }  // namespace dtd
 
 #define DTD_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -306,10 +306,10 @@ __device__ __forceinline__ void stage(const StageOffs& o, __amdgpu_buffer_rsrc_t
   for (int i = 0; i < 2; ++i) {
     if constexpr (H == 0 || H == 3) {
       constexpr int h = H == 3 ? 1 : 0;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(buf + o.la[h][i]), 16, o.a[h][i], so, 0, 0);
+      dma16(ra, buf + o.la[h][i], o.a[h][i], so);
     } else {
       constexpr int h = H == 2 ? 1 : 0;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(buf + o.lb[h][i]), 16, o.b[h][i], so, 0, 0);
+      dma16(rb, buf + o.lb[h][i], o.b[h][i], so);
     }
   }
 }
@@ -569,7 +569,7 @@ __device__ __forceinline__ void stage_tn(const TnOffs& oa0, const TnOffs& ob0, c
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     char* dst = buf + (isb ? A_BYTES : 0) + o.l[i];
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(isb ? rb : ra, (lds_void*)dst, 16, o.o[i], so, 0, 0);
+    dma16(isb ? rb : ra, dst, o.o[i], so);
   }
 }
 

@@ -135,14 +135,12 @@ __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
   auto dma_w = [&](int kt, int s) {
 #pragma unroll
     for (int j = 0; j < W_DMA; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(wl + s * W_STAGE + j * 16 * ROWB), 16, vw,
-                                               j * sw16 + kt * ROWB, 0, 0);
+      dma16(rw, wl + s * W_STAGE + j * 16 * ROWB, vw, j * sw16 + kt * ROWB);
   };
   auto dma_x = [&](int kt, int s) {
 #pragma unroll
     for (int j = 0; j < X_DMA; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void*)(xl + s * X_STAGE + j * 16 * ROWB), 16, vx,
-                                               j * sx16 + kt * ROWB, 0, 0);
+      dma16(rx, xl + s * X_STAGE + j * 16 * ROWB, vx, j * sx16 + kt * ROWB);
   };
 
   // ---- fragment reads: lane reads row (lane & 31) of a 32-row tile, 16-byte chunk 2 ks + (lane >> 5)
@@ -194,8 +192,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
       xf[j] = *reinterpret_cast<const bf16x8*>(xfr + (kt2 % 3) * X_STAGE + c + j * 32 * ROWB);
     };
     auto dma_x_one = [&](int j, int kx, int sx) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void*)(xl + sx * X_STAGE + j * 16 * ROWB), 16, vx,
-                                               j * sx16 + kx * ROWB, 0, 0);
+      dma16(rx, xl + sx * X_STAGE + j * 16 * ROWB, vx, j * sx16 + kx * ROWB);
     };
     // prologue: X(0), X(1), X(2) and the first half-step's weight fragments in flight
     dma_x(0, 0);
@@ -248,11 +245,9 @@ __global__ void __launch_bounds__(256, 1) gemm_ln_kernel(GemmLnArgs g) {
     // one 16-row DMA instruction / one fragment read, by index
     auto dma_one = [&](int j, int kw, int sw, int kx, int sx) {
       if (j < W_DMA)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(wl + sw * W_STAGE + j * 16 * ROWB), 16, vw,
-                                                 j * sw16 + kw * ROWB, 0, 0);
+        dma16(rw, wl + sw * W_STAGE + j * 16 * ROWB, vw, j * sw16 + kw * ROWB);
       else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void*)(xl + sx * X_STAGE + (j - W_DMA) * 16 * ROWB), 16,
-                                                 vx, (j - W_DMA) * sx16 + kx * ROWB, 0, 0);
+        dma16(rx, xl + sx * X_STAGE + (j - W_DMA) * 16 * ROWB, vx, (j - W_DMA) * sx16 + kx * ROWB);
     };
     auto read_one = [&](int j, int kt2, int c, bf16x8 (&wf)[FB], bf16x8 (&xf)[TB]) {
       if (j < TB) xf[j] = *reinterpret_cast<const bf16x8*>(xfr + (kt2 % 3) * X_STAGE + c + j * 32 * ROWB);

@@ -489,3 +489,37 @@ def wgrad_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) -> to
     _lib.call("dtd_gemm_tn", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), part.data_ptr(), o, i, T,
               splits, _lib.stream())
     return part
+
+
+# Weight gradients on the ring-pipelined TN kernel (ops/csrc/wgrad.hip), default on: DTD_WGRAD2=0
+# keeps them on hipBLASLt's split-K bmm (A/B runs).
+_WGRAD2 = [os.environ.get("DTD_WGRAD2", "1") == "1"]
+
+
+def wgrad2_enabled() -> bool:
+    return _ENABLED[0] and _WGRAD2[0]
+
+
+def set_wgrad2(on: bool) -> None:
+    _WGRAD2[0] = bool(on)
+
+
+def wgrad2_supported(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    """Contract of the ring-pipelined weight-gradient kernel (``ops/csrc/wgrad.hip``): dy [T, o],
+    x [T, i] bf16 row-major views on the GPU, o and i multiples of 256, T a multiple of 32."""
+    if not (_ok(dy) and _ok(x)) or dy.shape[0] != x.shape[0] or not _lib.has("dtd_wgrad_tn"):
+        return False
+    return bool(_lib.lib().dtd_wgrad_tn_supported(dy.shape[1], x.shape[1], dy.shape[0]))
+
+
+def wgrad2_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None, variant: int = 0) -> torch.Tensor:
+    """fp32 partials [splits, o, i] of dy^T x over contiguous token ranges (``wgrad.hip``:
+    LDS ring of 32-token stages, ``variant`` = ring depth 4 or 5, 0 = default)."""
+    T, o = dy.shape
+    i = x.shape[1]
+    if splits is None:
+        splits = _lib.lib().dtd_wgrad_tn_splits(o, i, T)
+    part = torch.empty((splits, o, i), dtype=torch.float32, device=dy.device)
+    _lib.call("dtd_wgrad_tn", variant, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), part.data_ptr(), o, i,
+              T, splits, _lib.stream())
+    return part

@@ -624,11 +624,11 @@ class ZeroEngine(nn.Module):
         """Reduce one segment's gradients: all-reduce (stage 0) or reduce-scatter into the
         local gradient shard (stages 1-3); stage 2/3 landing regions go back to the arena."""
         s.launched = True
-        for p in s.params:  # parameters without a gradient this step contribute zeros
-            if not p._dtd_touched and s.gbuf is not None:
-                p.main_grad.zero_()
-        if s.gbuf is None:
+        if s.gbuf is None:   # no parameter of this segment got a gradient yet: land it now
             self._alloc_landing(s)
+        for p in s.params:  # parameters without a gradient this step contribute zeros (the
+            if not p._dtd_touched:   # recycled landing region holds an earlier segment's bytes)
+                p.main_grad.zero_()
         buf = s.gbuf
         # stages 0/1 accumulate micro-batches in the full gradient buffer and reduce once;
         # stages 2/3 reduce every micro-batch and accumulate the shards
@@ -803,6 +803,14 @@ class ZeroEngine(nn.Module):
     def _reset(self) -> None:
         accumulate_full = (self.stage <= 1 or self.replicated) and self.micro_step > 0  # keep accumulating in place
         self.tracker.reset()
+        # a unit kept gathered by a training forward that had no backward (hold set in its
+        # post-forward hook, cleared only by its own reduce) would otherwise stay gathered into
+        # this step and skip the re-gather of the updated weights
+        for u in self.units:
+            if u.hold or u.pending_release:
+                u.hold = False
+                u.pending_release = False
+                self._release(u)
         self.landing.new_window()
         self.gather_arena.new_window()
         for s in self.segments:

@@ -69,11 +69,16 @@ def ddp_nosync_worker(rank, world, port, out_dir, impl):
 
 
 def zero_worker(rank, world, port, out_dir, model_name, stage, n_steps, gas, clip=0.0, tag="", force=False,
-                poison=False):
+                poison=False, unused=False):
     from distributed_training_and_deepspeed_amd.comm import logger as clog
     from distributed_training_and_deepspeed_amd.parallel.zero import initialize
     comm.init(rank=rank, world_size=world, backend="gloo", master_port=port)
     model = build_model(model_name, impl="fused", seed=3)
+    if unused:   # trainable parameters that never get a gradient: one on the model, one in a layer
+        g = torch.Generator().manual_seed(5)
+        model.register_parameter("unused_top", torch.nn.Parameter(torch.randn(1000, generator=g)))
+        layer = next(m for m in model.modules() if m is not model and any(True for _ in m.parameters()))
+        layer.register_parameter("unused_in_layer", torch.nn.Parameter(torch.randn(300, generator=g)))
     cfg = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": gas,
            "optimizer": {"type": "Adam", "params": {"lr": 1e-3}},
            "comms_logger": {"enabled": True, "prof_all": True},

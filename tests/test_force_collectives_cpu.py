@@ -65,6 +65,22 @@ def test_zero_force_collectives_world1(tmp_path):
             assert 0 < forced["landing_numel"] <= forced["grad_numel"]
 
 
+def test_zero_poisoned_landing_with_unused_parameters(tmp_path):
+    """Stages 2 and 3 with NaN-poisoned recycled landing bytes and parameters that never get a
+    gradient: the untouched parameters' landing ranges are zeroed before the reduce-scatter, so
+    every shard stays finite and equals the unpoisoned run's."""
+    for stage in (2, 3):
+        _spawn(W.zero_worker, 1, pick_free_port(), str(tmp_path), "causal-tiny", stage, 2, 1, 0.0, "_clean",
+               True, False, True)
+        _spawn(W.zero_worker, 1, pick_free_port(), str(tmp_path), "causal-tiny", stage, 2, 1, 0.0, "_poison",
+               True, True, True)
+        clean = torch.load(tmp_path / f"zero{stage}_clean.pt", weights_only=True)
+        pois = torch.load(tmp_path / f"zero{stage}_poison.pt", weights_only=True)
+        for a, b in zip(clean["shards"], pois["shards"]):
+            assert torch.isfinite(b).all(), stage
+            assert torch.equal(a, b), (stage, (a - b).abs().max().item())
+
+
 def test_ddp_tail_buckets_shape_bert_base():
     """Multi-GPU critical path: the embeddings (ready only when backward ends) get their own final
     bucket, and the first layer's gradients a small bucket just before it, so the all-reduce

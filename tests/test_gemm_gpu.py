@@ -139,6 +139,42 @@ def test_wgrad_tn_matches_fp32(T, o, i, splits):
     assert rel(dst - 1.0, ref) < 2e-3
 
 
+@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("T,o,i,splits", [(32, 256, 256, 1), (16384, 2304, 768, None), (16384, 768, 768, None),
+                                          (16384, 3072, 768, None), (16384, 768, 3072, None),
+                                          (4128, 512, 256, 7), (96, 256, 512, 8)])
+def test_wgrad2_tn_matches_fp32(T, o, i, splits, variant):
+    """Ring-pipelined TN weight-gradient kernel (ops/csrc/wgrad.hip) on every BERT-base weight
+    shape, uneven ranges (4128 tokens = 129 K-steps over 7 ranges) and ranges shorter than the
+    ring / empty ranges (96 tokens over 8), against an fp32 dy^T x."""
+    from distributed_training_and_deepspeed_amd.ops.grad import splitk_reduce
+    torch.manual_seed(7)
+    dy = torch.randn(T, o, device="cuda").bfloat16()
+    x = torch.randn(T, i, device="cuda").bfloat16()
+    assert G.wgrad2_supported(dy, x)
+    part = G.wgrad2_tn(dy, x, splits, variant=variant)
+    ref = dy.float().t() @ x.float()
+    assert rel(part.sum(0), ref) < 2e-3, rel(part.sum(0), ref)
+    dst = torch.full((o, i), 1.0, device="cuda", dtype=torch.float32)
+    splitk_reduce(part, dst, True)
+    assert rel(dst - 1.0, ref) < 2e-3
+
+
+@pytest.mark.parametrize("variant", [4, 5])
+def test_wgrad2_tn_asymmetric_and_strided(variant):
+    """I^T x = x exactly (a swapped accumulator map would return a transposed / permuted tile), on
+    column-sliced (strided) operands."""
+    T, n = 512, 256
+    big = torch.zeros(T, 3 * n, device="cuda").bfloat16()
+    big[:, n:2 * n] = torch.eye(n, device="cuda").bfloat16().repeat(T // n, 1)
+    dy = big[:, n:2 * n]
+    xb = torch.arange(T * 2 * n, device="cuda").float().view(T, 2 * n).remainder(13).bfloat16()
+    x = xb[:, n:]
+    part = G.wgrad2_tn(dy, x, 1, variant=variant)
+    ref = (dy.float().t() @ x.float())
+    assert torch.equal(part[0], ref)
+
+
 def test_wgrad_tn_asymmetric_detects_transpose():
     T, n = 256, 256
     dy = torch.eye(n, device="cuda").bfloat16().repeat(T // n, 1)          # [T, n]

@@ -24,11 +24,10 @@ import os
 
 # HIP hardware queues per process: the box default (4) is fewer than the streams of the N > 1
 # step (compute, keep-mask, optimizer, finalize and RCCL's own); streams sharing a queue
-# serialise their cross-stream waits.  Raised to 8 before anything initialises HIP
+# serialise their cross-stream waits.  Set to 8 (when unset) before anything initialises HIP
 # (docs/PERFORMANCE.md, "Hardware queues").
-_HWQ = os.environ.get("GPU_MAX_HW_QUEUES", "")
-if not _HWQ.isdigit() or int(_HWQ) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# A value the user set is kept as it is (e.g. 4 for an A/B run); the value in effect is logged.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 import sys
 import time
 
