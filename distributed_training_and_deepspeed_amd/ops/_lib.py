@@ -81,9 +81,6 @@ _SIGS = {
     "dtd_transpose_bf16": (I, [P, P, I, I, P]),
     "dtd_transpose_many": (I, [P, P, P, P, I, P]),
     "dtd_gemm_set_stamps": (I, [P]),
-    "dtd_gemm_tn_supported": (I, [I, I, I]),
-    "dtd_gemm_tn_splits": (I, [I, I, I]),
-    "dtd_gemm_tn": (I, [P, I, P, I, P, I, I, I, I, P]),
     # wgrad.hip
     "dtd_wgrad_tn_supported": (I, [I, I, I]),
     "dtd_wgrad_tn_splits": (I, [I, I, I]),

@@ -513,197 +513,6 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// TN form for weight gradients: P[split][M][N] = A[k0:k1, :M]^T . B[k0:k1, :N] with A [K][M] and
-// B [K][N] row-major (dW[o, i] = sum_t dY[t, o] X[t, i]: A = dY, B = X, K = tokens).  The
-// reduction runs down the rows, so an LDS K-step holds 64 token rows x 256 columns (512-byte
-// rows, 16-byte chunks XOR-swizzled by tn_swz(row)) and the MFMA operands are read with the
-// transposing ds_read_b64_tr_b16 (two 4-row reads per 8-deep fragment).  Phases follow the
-// K-half order (k0 rows 0-63 of the wave's M half, k0 rows 64-127, k1 64-127, k1 0-63), and the
-// DMA quarters A k0, B k0, A k1, B k1 are staged one K-step ahead in that order.  Each
-// workgroup owns one 256x256 tile and one contiguous K range (split-K: tiles x splits <= CUs,
-// a single wave of workgroups), writes fp32 partials, and ops/csrc/reduce.hip sums the splits.
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-__device__ __forceinline__ bf16x4 tr_read(const char* p) {
-  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
-  return __builtin_bit_cast(bf16x4, v);
-}
-
-// chunk swizzle of LDS row t: the 8 rows a 32-lane half of a transposing read touches
-// ({8g + q, 8g + 8 + q}, q = 0..3) land on 8 distinct 32-byte slots of the 256-byte bank window
-__device__ __forceinline__ int tn_swz(int t) { return ((t & 3) | (((t >> 3) & 1) << 2)) << 1; }
-
-struct TnArgs {
-  const bf16* a; const bf16* b;          // A [K][M] (lda), B [K][N] (ldb)
-  float* part;                           // [splits][M][N] fp32
-  int M, N, K, lda, ldb;
-  int splits, ksplit;                    // K-steps per split (the last split may be shorter)
-};
-
-struct TnOffs {
-  int o[2];   // per-lane byte offsets (row pair of DMA i, swizzled chunk) relative to a K-step base
-  int l[2];   // LDS byte offsets of the two row pairs within a 32-row quarter
-};
-
-__device__ __forceinline__ TnOffs tn_offsets(int w, int lane, int ld, int quarter_row0) {
-  TnOffs o;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = quarter_row0 + 2 * (w * 2 + i) + (lane >> 5);   // row of the K-step (0..63)
-    const int gchunk = (lane & 31) ^ tn_swz(r);
-    o.o[i] = (r * ld + gchunk * 8) * 2;
-    o.l[i] = (quarter_row0 + 2 * (w * 2 + i)) * 512;
-  }
-  return o;
-}
-
-// quarter Q of K-step kt (0: A rows 0-31, 1: B rows 0-31, 2: A rows 32-63, 3: B rows 32-63)
-template <int Q>
-__device__ __forceinline__ void stage_tn(const TnOffs& oa0, const TnOffs& ob0, const TnOffs& oa1, const TnOffs& ob1,
-                                         __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int lda, int ldb,
-                                         char* buf, int kt) {
-  constexpr bool isb = Q == 1 || Q == 3;
-  const TnOffs& o = Q == 0 ? oa0 : Q == 1 ? ob0 : Q == 2 ? oa1 : ob1;
-  const int so = kt * BK * (isb ? ldb : lda) * 2;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    char* dst = buf + (isb ? A_BYTES : 0) + o.l[i];
-    dma16(isb ? rb : ra, dst, o.o[i], so);
-  }
-}
-
-__global__ void __launch_bounds__(512, 2) gemm_tn_kernel(TnArgs g) {
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int li = lane & 15, lq = lane >> 4;
-  const int wm = w >> 2, wn = w & 3;
-  const int ntn = g.N / BN;
-  // XCD-aware order: each XCD runs a contiguous range of (split, tile) with the tile index minor,
-  // so the tiles of one split -- which all stream the same K rows of A and B -- share that
-  // XCD's L2.  In hardware order (tile-major over the splits) every XCD fetched every split's
-  // rows: ~(M/256 + N/256) x the operand bytes from HBM, which bounded the kernel (qkv wgrad:
-  // 3.6 GB in 0.58 ms).
-  const int ntiles = (g.M / BM) * (g.N / BN);
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = L % ntiles, sp = L / ntiles;
-  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
-  const int nk_all = g.K / BK;
-  const int kb = sp * g.ksplit;
-  const int nk = min(g.ksplit, nk_all - kb);
-  float* out = g.part + (size_t)sp * g.M * g.N;
-  if (nk <= 0) {   // empty split: zero partial tile (keeps the reduce a plain sum)
-    for (int i = tid; i < BM * BN / 4; i += 512) {
-      const int r = i / (BN / 4), c = (i % (BN / 4)) * 4;
-      *reinterpret_cast<f32x4*>(out + (size_t)(m0 + r) * g.N + n0 + c) = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    return;
-  }
-  const TnOffs oa0 = tn_offsets(w, lane, g.lda, 0), oa1 = tn_offsets(w, lane, g.lda, 32);
-  const TnOffs ob0 = tn_offsets(w, lane, g.ldb, 0), ob1 = tn_offsets(w, lane, g.ldb, 32);
-  const auto ra = uniform_rsrc(g.a + (size_t)kb * BK * g.lda + m0);
-  const auto rb = uniform_rsrc(g.b + (size_t)kb * BK * g.ldb + n0);
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  stage_tn<0>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, smem, 0);
-  stage_tn<1>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, smem, 0);
-  stage_tn<2>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, smem, 0);
-  stage_tn<3>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, smem, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (__builtin_amdgcn_readfirstlane(wm) == 1) bar();   // stagger wave row 1
-
-  // transposing-read lane geometry: group gq = lane >> 4 reads rows 8 gq + (li >> 2) (+4), the
-  // 4 columns 4 (li & 3) .. + 3 of a 16-column block; lane receives column li of those rows
-  const int trow = 8 * lq + (li >> 2);
-  const int tcol = 4 * (li & 3);
-  // The swizzle of every row this lane reads (ks * 32 + trow, + 4) depends on row bits 0, 1 and
-  // 3 only -- one lane constant -- so the 12 swizzled operand offsets are computed once and each
-  // transposing read is base + immediate (per-read XOR / shift address math in the phases kept
-  // the partner wave's MFMAs waiting).
-  const int sw = tn_swz(trow);
-  int aoff[8], boff[4];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int col = wm * 128 + c * 16 + tcol;
-    aoff[c] = trow * 512 + (((col >> 3) ^ sw) << 4) + (col & 7) * 2;
-  }
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int col = wn * 64 + ni * 16 + tcol;
-    boff[ni] = trow * 512 + A_BYTES + (((col >> 3) ^ sw) << 4) + (col & 7) * 2;
-  }
-  bf16x8 af[4], bk[4];
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = smem + (kt & 1) * TILE_BYTES;
-    char* nxt = smem + ((kt & 1) ^ 1) * TILE_BYTES;
-    const bool more = kt + 1 < nk;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int ks = p >> 1, qm = (p == 1 || p == 2) ? 1 : 0;
-      {
-        const char* r0 = cur + ks * 32 * 512;   // rows ks*32 + trow (in the offsets) and + 4
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const char* q = r0 + aoff[qm * 4 + mi];
-          af[mi] = __builtin_shufflevector(tr_read(q), tr_read(q + 4 * 512), 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-        if (p == 0 || p == 2) {
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            const char* q = r0 + boff[ni];
-            bk[ni] = __builtin_shufflevector(tr_read(q), tr_read(q + 4 * 512), 0, 1, 2, 3, 4, 5, 6, 7);
-          }
-        }
-      }
-      // Counted waits retire exactly what this phase reads (2 LDS-DMA instructions per quarter,
-      // completing in issue order): phase 0 needs quarters 0 and 1 of this K-step, phase 1
-      // quarter 0, phase 2 quarters 2 and 3, phase 3 quarter 2.  With the next K-step's quarter
-      // p issued first, that leaves 3 / 4 / 3 / 5 quarters in flight (a blanket vmcnt(4) made
-      // every quarter land 2 phases after issue, which the strided row DMA often did not).
-      if (more) {
-        if (p == 0) stage_tn<0>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, nxt, kt + 1);
-        if (p == 1) stage_tn<1>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, nxt, kt + 1);
-        if (p == 2) stage_tn<2>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, nxt, kt + 1);
-        if (p == 3) stage_tn<3>(oa0, ob0, oa1, ob1, ra, rb, g.lda, g.ldb, nxt, kt + 1);
-        if (p == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        if (p == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        if (p == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        if (p == 3) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      } else if (p <= 1) {
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      bar();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[qm * 4 + mi][ni] = mfma16(bk[ni], af[mi], acc[qm * 4 + mi][ni]);
-      __builtin_amdgcn_s_setprio(0);
-      bar();
-    }
-  }
-  if (__builtin_amdgcn_readfirstlane(wm) == 0) bar();   // close the stagger
-
-  // fp32 partial tile straight from the accumulators: lane holds P[m][n .. n+3] (16 bytes)
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-      *reinterpret_cast<f32x4*>(out + (size_t)(m0 + wm * 128 + mi * 16 + li) * g.N + n0 + wn * 64 + ni * 16 +
-                                4 * lq) = acc[mi][ni];
-}
-
-// ---------------------------------------------------------------------------------------------
 // Persistent form: one 512-thread workgroup per CU walks its tiles (XCD group x = blockIdx % 8
 // owns a contiguous tile range, its 32 workgroups take every 32nd tile of it, so the tiles in
 // flight on one XCD share A panels).  The K-step stream never drains between tiles: the last
@@ -1237,32 +1046,6 @@ DTD_EXPORT int dtd_spin_occupy(int nwg, double us, hipStream_t s) {
   DTD_LAUNCH_CHECK();
 }
 
-// Weight-gradient product (TN): part[s] = A[k_s]^T B[k_s] over `splits` contiguous K ranges of
-// whole 64-row K-steps; A [K][M], B [K][N] bf16 row-major; part fp32 [splits][M][N].
-// Shape contract: M, N % 256 == 0, K % 64 == 0, lda >= M, ldb >= N, lda / ldb % 8 == 0.
-DTD_EXPORT int dtd_gemm_tn_supported(int M, int N, int K) {
-  return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0;
-}
-
-// split count for a TN product: one wave of workgroups over the CUs
-DTD_EXPORT int dtd_gemm_tn_splits(int M, int N, int K) {
-  const int tiles = (M / BM) * (N / BN), nk = K / BK;
-  int s = num_cus() / tiles;
-  if (s < 1) s = 1;
-  if (s > nk) s = nk;
-  return s;
-}
-
-DTD_EXPORT int dtd_gemm_tn(const void* a, int lda, const void* b, int ldb, float* part, int M, int N, int K,
-                           int splits, hipStream_t s) {
-  if (!dtd_gemm_tn_supported(M, N, K) || splits < 1) return (int)hipErrorInvalidValue;
-  if ((lda | ldb) % 8 || lda < M || ldb < N) return (int)hipErrorInvalidValue;
-  const int nk = K / BK, ksplit = (nk + splits - 1) / splits;
-  TnArgs g{(const bf16*)a, (const bf16*)b, part, M, N, K, lda, ldb, splits, ksplit};
-  const int ntiles = (M / BM) * (N / BN);
-  hipLaunchKernelGGL(gemm_tn_kernel, dim3(ntiles * splits), dim3(512), 0, s, g);
-  DTD_LAUNCH_CHECK();
-}
 
 // ins[i] [rows[i]][cols[i]] -> outs[i] [cols[i]][rows[i]] for i < n in one launch (vector form only:
 // rows, cols multiples of 8, 16-byte aligned pointers; n <= 64)

@@ -17,8 +17,9 @@ input-gradient product uses the transposed weight, ``transpose``):
                                       backward partner of ``linear_act_grad``: a multiply instead of
                                       the derivative's transcendental math)
 * ``wgrad_tn(dy, x)``              -> fp32 split-K partials of dy^T x (weight gradient of a Linear:
-                                      both operands row-major over the token dim, transposing LDS
-                                      reads; one wave of workgroups; ``grad.splitk_reduce`` sums)
+                                      both operands row-major over the token dim; ``ops/csrc/wgrad.hip``,
+                                      a ring-pipelined TN kernel with transposing LDS reads; one wave
+                                      of workgroups; ``grad.splitk_reduce`` sums)
 
 The kernel is the 256x256 8-phase LDS-DMA pipeline of cdna_hip_programming.md §5 (see the .hip
 header).  Shapes must tile by 256 x 256 x 64 (``supported``); callers fall back to hipBLASLt +
@@ -56,11 +57,10 @@ _FFN_BWD = [os.environ.get("DTD_GEMM_FFN_BWD", "1") == "1"]
 # The FFN up-projection stores gelu'(u) instead of u (the derivative's exp / rcp shared with the
 # forward GELU; the backward epilogue is a multiply).  One extra bf16 rounding of the derivative.
 _FFN_STORE_GRAD = [os.environ.get("DTD_GEMM_FFN_STORE_GRAD", "1") == "1"]
-# TN weight-gradient kernel: off by default -- even on the o-projection, where it wins in
-# isolation, the full-chip split-K grid on the side stream cost 0.35 % end-to-end
-# (profiles/r2_ab_gemm_oproj.jsonl).  The NT kernel on the transposed o-projection weight (152 vs
-# 164 us in isolation) was neutral end-to-end as well and is not wired in.
-_WGRAD = [os.environ.get("DTD_GEMM_WGRAD", "0") == "1"]
+# Weight gradients on the ring-pipelined TN kernel (ops/csrc/wgrad.hip), default on: 1.2-1.29 PF/s
+# against the library split-K bmm's 0.89-1.05 on the BERT-base weights (profiles/r5_s2_wgrad.jsonl),
+# +4.6 % whole step (profiles/r5_s3_results.jsonl).  DTD_GEMM_WGRAD=0 keeps them on hipBLASLt.
+_WGRAD = [os.environ.get("DTD_GEMM_WGRAD", "1") == "1"]
 # DTD_GEMM_ALL=1: every transformer-layer projection on the hand-written kernels -- forward
 # (gemm_bt + bias), input gradients (gemm_bt on the transposed weight), weight gradients (TN
 # kernel, fp32 split-K partials) -- no vendor GEMM in the layers.  Off by default: the NT main loop
@@ -95,6 +95,10 @@ def ffn_store_grad_enabled() -> bool:
 
 def wgrad_enabled() -> bool:
     return _ENABLED[0] and (_WGRAD[0] or _ALL[0])
+
+
+def set_wgrad(on: bool) -> None:
+    _WGRAD[0] = bool(on)
 
 
 def all_enabled() -> bool:
@@ -463,58 +467,17 @@ def dgrad_add_(c: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> torch.Tens
     return c.addmm_(dy, wt.t())
 
 
-def wgrad_preferred(o: int, i: int) -> bool:
-    """Where the TN kernel beats hipBLASLt's split-K bmm: small weights (<= 16 output tiles of
-    256 x 256, e.g. the 768 x 768 attention output projection: 165 vs 176 us at 131k tokens).  Its
-    transposing-read main loop runs ~0.85 PF/s, below hipBLASLt on the larger weights
-    (profiles/r2_gemm8_vs_hipblaslt.jsonl), so those stay on the library (all of them take the
-    kernel in the all-native mode)."""
-    return _ALL[0] or (o // 256) * (i // 256) <= 16
-
-
 def wgrad_supported(dy: torch.Tensor, x: torch.Tensor) -> bool:
-    """dy [T, o], x [T, i] bf16 row-major views on the GPU with o, i % 256 == 0, T % 64 == 0."""
-    if not (_ok(dy) and _ok(x)) or dy.shape[0] != x.shape[0] or not _lib.has("dtd_gemm_tn"):
-        return False
-    return bool(_lib.lib().dtd_gemm_tn_supported(dy.shape[1], x.shape[1], dy.shape[0]))
-
-
-def wgrad_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
-    """fp32 partials [splits, o, i] of dy^T x over contiguous token ranges."""
-    T, o = dy.shape
-    i = x.shape[1]
-    if splits is None:
-        splits = _lib.lib().dtd_gemm_tn_splits(o, i, T)
-    part = torch.empty((splits, o, i), dtype=torch.float32, device=dy.device)
-    _lib.call("dtd_gemm_tn", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), part.data_ptr(), o, i, T,
-              splits, _lib.stream())
-    return part
-
-
-# Weight gradients on the ring-pipelined TN kernel (ops/csrc/wgrad.hip), default on: DTD_WGRAD2=0
-# keeps them on hipBLASLt's split-K bmm (A/B runs).
-_WGRAD2 = [os.environ.get("DTD_WGRAD2", "1") == "1"]
-
-
-def wgrad2_enabled() -> bool:
-    return _ENABLED[0] and _WGRAD2[0]
-
-
-def set_wgrad2(on: bool) -> None:
-    _WGRAD2[0] = bool(on)
-
-
-def wgrad2_supported(dy: torch.Tensor, x: torch.Tensor) -> bool:
-    """Contract of the ring-pipelined weight-gradient kernel (``ops/csrc/wgrad.hip``): dy [T, o],
-    x [T, i] bf16 row-major views on the GPU, o and i multiples of 256, T a multiple of 32."""
+    """Contract of the weight-gradient kernel (``ops/csrc/wgrad.hip``): dy [T, o], x [T, i] bf16
+    row-major views on the GPU, o and i multiples of 256, T a multiple of 32."""
     if not (_ok(dy) and _ok(x)) or dy.shape[0] != x.shape[0] or not _lib.has("dtd_wgrad_tn"):
         return False
     return bool(_lib.lib().dtd_wgrad_tn_supported(dy.shape[1], x.shape[1], dy.shape[0]))
 
 
-def wgrad2_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None, variant: int = 0) -> torch.Tensor:
-    """fp32 partials [splits, o, i] of dy^T x over contiguous token ranges (``wgrad.hip``:
-    LDS ring of 32-token stages, ``variant`` = ring depth 4 or 5, 0 = default)."""
+def wgrad_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None, variant: int = 0) -> torch.Tensor:
+    """fp32 partials [splits, o, i] of dy^T x over contiguous token ranges (``wgrad.hip``: LDS ring
+    of 32-token stages; ``variant`` = ring depth 4 or 5, 0 = the default depth)."""
     T, o = dy.shape
     i = x.shape[1]
     if splits is None:

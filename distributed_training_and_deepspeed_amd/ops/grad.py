@@ -201,14 +201,10 @@ def _emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
             return
     if dy.is_cuda and T >= 8192:
         from . import gemm as G
-        if G.wgrad2_enabled() and G.wgrad2_supported(dy, x):
+        if G.wgrad_enabled() and G.wgrad_supported(dy, x):
             # ring-pipelined TN MFMA kernel (ops/csrc/wgrad.hip): fp32 split-K partials, one wave
             # of workgroups, 1.2-1.29 PF/s on the BERT-base weights at 131k tokens against the
             # library's 0.89-1.05 (profiles/r5_s2_wgrad.jsonl)
-            splitk_reduce(G.wgrad2_tn(dy, x), dst, acc)
-            return
-        if G.wgrad_enabled() and G.wgrad_preferred(o, i) and G.wgrad_supported(dy, x):
-            # hand-written TN MFMA GEMM: fp32 split-K partials in one wave of workgroups
             splitk_reduce(G.wgrad_tn(dy, x), dst, acc)
             return
     s = wgrad_splits(T, o, i) if dy.is_cuda else 1

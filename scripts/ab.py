@@ -95,7 +95,7 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "opt_overlap_off": lambda: ["--opt-overlap", "off"], "gemm_sched_static": _env(DTD_GEMM_SCHED="static"),
            "no_fused_embed_ln": _env(DTD_FUSED_EMBED_LN="0"), "no_fused_xent": _env(DTD_FUSED_XENT="0"), "fused_xent": _env(DTD_FUSED_XENT="1"), "no_defer_finalize": _env(DTD_DEFER_FINALIZE="0"),
            "gemm_stagger2": _env(DTD_GEMM_STAGGER_US="2"), "gemm_stagger4": _env(DTD_GEMM_STAGGER_US="4"),
-           "attn_bwd_fused": _env(DTD_ATTN_BWD="fused"), "no_wgrad2": _env(DTD_WGRAD2="0"),
+           "attn_bwd_fused": _env(DTD_ATTN_BWD="fused"), "no_wgrad2": _env(DTD_GEMM_WGRAD="0"),
            "dmabuiltin_so": _env(DTD_KERNELS_SO=os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops",
                                                             "_dtd_kernels_dmabuiltin.so")),
            "b320": lambda: ["--batch-size", "320"], "b384": lambda: ["--batch-size", "384"],

@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """Weight-gradient GEMMs of a BERT-base layer at bench.py's token count: the production library
-path (hipBLASLt split-K bmm, TunableOp-tuned, + splitk_reduce), the round-2/3 TN kernel
-(ops/csrc/gemm.hip gemm_tn_kernel) and the ring-pipelined TN kernel (ops/csrc/wgrad.hip) at each
-ring depth.  Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24); one JSON
+path (hipBLASLt split-K bmm, TunableOp-tuned, + splitk_reduce) and the ring-pipelined TN kernel
+(ops/csrc/wgrad.hip) at each ring depth (profiles/r5_s2_wgrad.jsonl also has the round-2/3
+TN kernel, since removed, as "tn_r3").  Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24); one JSON
 line per shape with median us, TF/s and the error of each path against an fp32 reference.
 
     T=131072 ROUNDS=5 python scripts/bench_wgrad.py
@@ -57,11 +57,10 @@ def main():
             a, b = dy.view(s, T // s, o).transpose(1, 2), xx.view(s, T // s, i)
             GR.splitk_reduce(GR._bmm_partials(a, b, fp32=False), dst, False)
 
-        paths = {"hipblaslt": lib,
-                 "tn_r3": lambda: GR.splitk_reduce(G.wgrad_tn(dy, xx), dst, False)}
+        paths = {"hipblaslt": lib}
         for v in variants:
-            paths[f"ring{v}"] = lambda v=v: GR.splitk_reduce(G.wgrad2_tn(dy, xx, variant=v), dst, False)
-            paths[f"ring{v}_kernel"] = lambda v=v: G.wgrad2_tn(dy, xx, variant=v)
+            paths[f"ring{v}"] = lambda v=v: GR.splitk_reduce(G.wgrad_tn(dy, xx, variant=v), dst, False)
+            paths[f"ring{v}_kernel"] = lambda v=v: G.wgrad_tn(dy, xx, variant=v)
         ref = dy.float().t() @ xx.float()
         err = {}
         for k, f in paths.items():

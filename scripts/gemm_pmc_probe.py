@@ -32,7 +32,7 @@ def run():
 
 def run_wgrad():
     """fc1 weight gradient (dW [3072, 768] = dU^T X over T = 131072 tokens): the TN kernel's fp32
-    split-K partials vs hipBLASLt's 16-slice bmm (the model's default), three launches each."""
+    split-K partials (ops/csrc/wgrad.hip) vs hipBLASLt's 16-slice bmm, three launches each."""
     from distributed_training_and_deepspeed_amd.ops import gemm as G
     from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
     use_tuned_gemms()
@@ -51,7 +51,8 @@ def summarize(paths):
     for path in paths:
         for r in csv.DictReader(open(path)):
             name = r.get("Kernel_Name", "")
-            fam = "ours" if ("gemm_bt" in name or "gemm_tn" in name) else ("hipblaslt" if "Cijk" in name else None)
+            fam = ("ours" if ("gemm_bt" in name or "gemm_tn" in name or "wgrad_tn" in name)
+                   else ("hipblaslt" if "Cijk" in name else None))
             if fam is None:
                 continue
             grid = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)

@@ -143,7 +143,7 @@ def test_wgrad_tn_matches_fp32(T, o, i, splits):
 @pytest.mark.parametrize("T,o,i,splits", [(32, 256, 256, 1), (16384, 2304, 768, None), (16384, 768, 768, None),
                                           (16384, 3072, 768, None), (16384, 768, 3072, None),
                                           (4128, 512, 256, 7), (96, 256, 512, 8)])
-def test_wgrad2_tn_matches_fp32(T, o, i, splits, variant):
+def test_wgrad_tn_ring_matches_fp32(T, o, i, splits, variant):
     """Ring-pipelined TN weight-gradient kernel (ops/csrc/wgrad.hip) on every BERT-base weight
     shape, uneven ranges (4128 tokens = 129 K-steps over 7 ranges) and ranges shorter than the
     ring / empty ranges (96 tokens over 8), against an fp32 dy^T x."""
@@ -151,8 +151,8 @@ def test_wgrad2_tn_matches_fp32(T, o, i, splits, variant):
     torch.manual_seed(7)
     dy = torch.randn(T, o, device="cuda").bfloat16()
     x = torch.randn(T, i, device="cuda").bfloat16()
-    assert G.wgrad2_supported(dy, x)
-    part = G.wgrad2_tn(dy, x, splits, variant=variant)
+    assert G.wgrad_supported(dy, x)
+    part = G.wgrad_tn(dy, x, splits, variant=variant)
     ref = dy.float().t() @ x.float()
     assert rel(part.sum(0), ref) < 2e-3, rel(part.sum(0), ref)
     dst = torch.full((o, i), 1.0, device="cuda", dtype=torch.float32)
@@ -161,7 +161,7 @@ def test_wgrad2_tn_matches_fp32(T, o, i, splits, variant):
 
 
 @pytest.mark.parametrize("variant", [4, 5])
-def test_wgrad2_tn_asymmetric_and_strided(variant):
+def test_wgrad_tn_asymmetric_and_strided(variant):
     """I^T x = x exactly (a swapped accumulator map would return a transposed / permuted tile), on
     column-sliced (strided) operands."""
     T, n = 512, 256
@@ -170,7 +170,7 @@ def test_wgrad2_tn_asymmetric_and_strided(variant):
     dy = big[:, n:2 * n]
     xb = torch.arange(T * 2 * n, device="cuda").float().view(T, 2 * n).remainder(13).bfloat16()
     x = xb[:, n:]
-    part = G.wgrad2_tn(dy, x, 1, variant=variant)
+    part = G.wgrad_tn(dy, x, 1, variant=variant)
     ref = (dy.float().t() @ x.float())
     assert torch.equal(part[0], ref)
 
@@ -184,11 +184,12 @@ def test_wgrad_tn_asymmetric_detects_transpose():
 
 
 def test_tn_wgrad_path_in_model_matches_default():
-    """The opt-in TN weight-gradient kernel (DTD_GEMM_WGRAD=1; taken for the small o-projection
-    weight at >= 8192 tokens) gives the same gradients as the default hipBLASLt split-K path."""
+    """The TN weight-gradient kernel (default; taken for every layer weight at >= 8192 tokens)
+    gives the same gradients as the hipBLASLt split-K path (DTD_GEMM_WGRAD=0)."""
     from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
     from distributed_training_and_deepspeed_amd.models import build_model
     grads = []
+    prev = G._WGRAD[0]
     for on in (False, True):
         G._WGRAD[0] = on
         try:
@@ -198,7 +199,7 @@ def test_tn_wgrad_path_in_model_matches_default():
             torch.cuda.synchronize()
             grads.append({n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None})
         finally:
-            G._WGRAD[0] = False
+            G._WGRAD[0] = prev
     assert grads[0].keys() == grads[1].keys()
     for n in grads[0]:
         g0, g1 = grads[0][n], grads[1][n]

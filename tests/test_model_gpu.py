@@ -234,7 +234,8 @@ def test_all_native_gemm_mode_matches_library_gemms(monkeypatch):
     # gradients through gemm_bt and the residual qkv one in the in-place EPI_ADD form (fc2's is
     # the fused GELU-backward kernel in both modes), 4 weight gradients through the TN kernel
     assert calls["bt"] - base["bt"] >= 6 * L, (base, calls)
-    assert calls["tn"] - base["tn"] >= 4 * L, (base, calls)
+    # the weight gradients take the TN kernel in both modes (it is the default path)
+    assert base["tn"] >= 4 * L and calls["tn"] - base["tn"] >= 4 * L, (base, calls)
     assert abs(out[0][0] - out[1][0]) <= 1e-2 * abs(out[0][0])
     g0, g1 = out[0][1], out[1][1]
     assert (g0 - g1).norm().item() <= 2e-2 * g0.norm().item()
