@@ -253,10 +253,14 @@ __host__ __device__ __forceinline__ uint32_t keep_threshold(float p) {
 // waits stricter: the counter retires in issue order).  M0 is set inside the statement (the
 // compiler does not preserve it around asm) and restored after it; the s_nop covers the
 // M0-write -> LDS-DMA hazard.
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
-  // the LDS base and scalar offset must be wave-uniform (SGPR operands): readfirstlane makes that
-  // provable where the caller's expression is not (a no-op on values already in SGPRs)
-  const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds);
+// LDS byte address of a pointer into a __shared__ array (32-bit, wave-uniform)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p);
+}
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint32_t lds, int voff, int soff) {
+  // the LDS address and the scalar offset must be wave-uniform (SGPR operands): readfirstlane makes
+  // that provable where the caller's expression is not (a no-op on values already in SGPRs)
+  const uint32_t m = __builtin_amdgcn_readfirstlane(lds);
   soff = __builtin_amdgcn_readfirstlane(soff);
 #ifdef DTD_DMA_BUILTIN   // A/B builds only: the builtin form (hipcc's drains included)
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(uintptr_t)m, 16, voff, soff,
@@ -267,6 +271,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds,
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
                "s_mov_b32 m0, %0"
                : "=&s"(keep) : "s"(m), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
+  dma16(r, lds_addr(lds), voff, soff);
 }
 
 }  // namespace dtd

@@ -103,9 +103,11 @@ template <int N> __device__ __forceinline__ void wait_vm() { asm volatile("s_wai
 // issued after barrier kt (spread over that K-step's MFMAs) fetches K-step kt + NBUF - 1 into the
 // buffer of K-step kt - 1.  At barrier kt the wave needs K-step kt + 1 and keeps the NBUF - 3
 // younger K-steps in flight.
-template <int NBUF>
+// DIAG (timing-only builds, wrong results unless 0): 1 = no LDS-DMA in the K loop (stale stages),
+// 2 = no barrier in the K loop, 4 = no fragment reads in the K loop (stale registers)
+template <int NBUF, bool UNROLL, int DIAG = 0>
 __global__ void __launch_bounds__(512, 2) wgrad_tn_kernel(WgArgs g) {
-  static_assert(NBUF >= 4 && NBUF <= 5, "ring depth");
+  static_assert(NBUF >= 4 && NBUF <= 5 && (!UNROLL || NBUF == 4), "ring depth");
   constexpr int DMA = 4;                    // LDS-DMA instructions per wave per K-step
   constexpr int KEEP = (NBUF - 3) * DMA;    // vmcnt that retires K-step kt+1 at barrier kt
   __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
@@ -142,8 +144,9 @@ __global__ void __launch_bounds__(512, 2) wgrad_tn_kernel(WgArgs g) {
   const auto rb = uniform_rsrc(g.b + (size_t)kb * BK * g.ldb + n0);
   const int sa = BK * g.lda * 2, sb = BK * g.ldb * 2;   // bytes per K-step
   // DMA piece i (0..3: A pair 0, B pair 0, A pair 1, B pair 1) of K-step kt into buffer base `buf`
-  auto dma = [&](char* buf, int kt, int i) {
-    char* dst = buf + (i >> 1 ? PANEL : 0) + (4 * w + 2 * (i & 1)) * ROWB;
+  const uint32_t lds0 = lds_addr(smem) + 4 * w * ROWB;   // this wave's first staged row
+  auto dma = [&](int buf, int kt, int i) {                // buf: byte offset of the stage
+    const uint32_t dst = lds0 + buf + (i >> 1 ? PANEL : 0) + 2 * (i & 1) * ROWB;
     if (i >> 1) dma16(rb, dst, vob[i & 1], kt * sb);
     else dma16(ra, dst, voa[i & 1], kt * sa);
   };
@@ -174,7 +177,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_tn_kernel(WgArgs g) {
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s) {
 #pragma unroll
-    for (int i = 0; i < DMA; ++i) dma(smem + s * STAGE, min(s, nk - 1), i);
+    for (int i = 0; i < DMA; ++i) dma(s * STAGE, min(s, nk - 1), i);
   }
   wait_vm<(NBUF - 2) * DMA>();
   bar();
@@ -189,39 +192,74 @@ __global__ void __launch_bounds__(512, 2) wgrad_tn_kernel(WgArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int cur = 0;   // byte offset of K-step kt's buffer
   // One K-step.  MFMA group mi (4 MFMAs on A fragment mi and the 4 B fragments of this K-step)
   // runs while the wave reads A fragment mi + 2 (of the next K-step for mi >= 6), half of a B
   // fragment of the next K-step (odd mi), and issues one DMA piece (mi < 4).  Nothing in the body
   // branches: past the range the DMA re-loads the range's last K-step into the free buffer and
-  // the last K-step's reads of the "next" buffer are discarded.
-  auto kstep = [&](auto par_c, int kt) {
+  // the last K-step's reads of the "next" buffer are discarded.  cur / nxt / prv: byte offsets of
+  // the buffers of K-steps kt, kt+1, kt-1 (compile-time constants in the unrolled form, so every
+  // fragment read is a lane-offset register plus an immediate: no address VALU per K-step).
+  auto kstep = [&](auto par_c, int kt, int cur, int nxt, int prv) {
     constexpr int PAR = decltype(par_c)::value;
     bf16x8 (&bc)[4] = PAR ? b1 : b0;
     bf16x8 (&bn)[4] = PAR ? b0 : b1;
-    const int nxt = cur + STAGE == NBUF * STAGE ? 0 : cur + STAGE;
-    const int prv = cur == 0 ? (NBUF - 1) * STAGE : cur - STAGE;
     const int issue_k = min(kt + NBUF - 1, nk - 1);
-    wait_vm<KEEP>();
+    if constexpr (!(DIAG & 1)) wait_vm<KEEP>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
+    if constexpr (!(DIAG & 2)) bar();
     const char* cb = smem + cur;
     const char* nb = smem + nxt;
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
-      if (mi < 6) a[(mi + 2) & 3] = frag(cb + aoff(mi + 2));
-      else a[(mi + 2) & 3] = frag(nb + aoff(mi - 6));
-      if (mi & 1) bn[mi >> 1] = frag(nb + boff(mi >> 1));
-      if (mi < DMA) dma(smem + prv, issue_k, mi);
+      if constexpr (!(DIAG & 4)) {
+        if (mi < 6) a[(mi + 2) & 3] = frag(cb + aoff(mi + 2));
+        else a[(mi + 2) & 3] = frag(nb + aoff(mi - 6));
+        if (mi & 1) bn[mi >> 1] = frag(nb + boff(mi >> 1));
+      } else {   // keep the registers live without reads
+        asm volatile("" : "+v"(a[(mi + 2) & 3]));
+        if (mi & 1) asm volatile("" : "+v"(bn[mi >> 1]));
+      }
+      if (!(DIAG & 1) && mi < DMA) dma(prv, issue_k, mi);
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(bc[ni], a[mi & 3], acc[mi][ni]);
+      // keep each group's reads in their group: left alone the scheduler sinks a read down to the
+      // MFMA group right before its consumer and exposes the LDS latency
+      __builtin_amdgcn_sched_barrier(0);
     }
-    cur = nxt;
   };
 
-  for (int kt = 0; kt < nk; kt += 2) {
-    kstep(std::integral_constant<int, 0>{}, kt);
-    if (kt + 1 < nk) kstep(std::integral_constant<int, 1>{}, kt + 1);
+  if constexpr (UNROLL) {
+    static_assert(NBUF % 2 == 0, "the B fragment parity follows the buffer index");
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    for (int kt = 0; kt < nk; kt += NBUF) {
+      kstep(P0{}, kt, 0, STAGE, (NBUF - 1) * STAGE);
+      if (kt + 1 >= nk) break;
+      kstep(P1{}, kt + 1, STAGE, 2 * STAGE, 0);
+      if (kt + 2 >= nk) break;
+      kstep(P0{}, kt + 2, 2 * STAGE, 3 * STAGE % (NBUF * STAGE), STAGE);
+      if (kt + 3 >= nk) break;
+      kstep(P1{}, kt + 3, 3 * STAGE, 4 * STAGE % (NBUF * STAGE), 2 * STAGE);
+      if constexpr (NBUF == 6) {
+        if (kt + 4 >= nk) break;
+        kstep(P0{}, kt + 4, 4 * STAGE, 5 * STAGE, 3 * STAGE);
+        if (kt + 5 >= nk) break;
+        kstep(P1{}, kt + 5, 5 * STAGE, 0, 4 * STAGE);
+      }
+    }
+  } else {
+    int cur = 0;
+    for (int kt = 0; kt < nk; kt += 2) {
+      int nxt = cur + STAGE == NBUF * STAGE ? 0 : cur + STAGE;
+      int prv = cur == 0 ? (NBUF - 1) * STAGE : cur - STAGE;
+      kstep(std::integral_constant<int, 0>{}, kt, cur, nxt, prv);
+      cur = nxt;
+      if (kt + 1 >= nk) break;
+      nxt = cur + STAGE == NBUF * STAGE ? 0 : cur + STAGE;
+      prv = cur == 0 ? (NBUF - 1) * STAGE : cur - STAGE;
+      kstep(std::integral_constant<int, 1>{}, kt + 1, cur, nxt, prv);
+      cur = nxt;
+    }
   }
   wait_vm<0>();   // no LDS-DMA may land after the workgroup has released its LDS
 
@@ -261,7 +299,7 @@ DTD_EXPORT int dtd_wgrad_tn_splits(int M, int N, int K) {
   return s < 1 ? 1 : s;
 }
 
-// variant: LDS ring depth (4 or 5); 0 = default
+// variant: LDS ring depth (4 or 5; 44 = depth 4, K loop unrolled by the ring); 0 = default
 DTD_EXPORT int dtd_wgrad_tn(int variant, const void* a, int lda, const void* b, int ldb, void* part, int M, int N,
                             int K, int splits, hipStream_t s) {
   if (!dtd_wgrad_tn_supported(M, N, K) || splits < 1) return (int)hipErrorInvalidValue;
@@ -271,10 +309,16 @@ DTD_EXPORT int dtd_wgrad_tn(int variant, const void* a, int lda, const void* b, 
   const int ksplit = (nk + splits - 1) / splits;
   WgArgs g{(const bf16*)a, (const bf16*)b, (float*)part, M, N, K, lda, ldb, splits, ksplit};
   const int nwg = (M / BM) * (N / BN) * splits;
-  if (variant == 0) variant = 4;   // 128 KiB: leaves LDS for a co-resident side-stream kernel
+  if (variant == 0) variant = 44;   // 128 KiB: leaves LDS for a co-resident side-stream kernel
   switch (variant) {
-    case 4: hipLaunchKernelGGL((wgrad_tn_kernel<4>), dim3(nwg), dim3(512), 0, s, g); break;
-    case 5: hipLaunchKernelGGL((wgrad_tn_kernel<5>), dim3(nwg), dim3(512), 0, s, g); break;
+    case 4: hipLaunchKernelGGL((wgrad_tn_kernel<4, false>), dim3(nwg), dim3(512), 0, s, g); break;
+    case 5: hipLaunchKernelGGL((wgrad_tn_kernel<5, false>), dim3(nwg), dim3(512), 0, s, g); break;
+    case 44: hipLaunchKernelGGL((wgrad_tn_kernel<4, true>), dim3(nwg), dim3(512), 0, s, g); break;
+    // diagnostic (timing-only) builds of variant 44: 440 + DIAG
+    case 441: hipLaunchKernelGGL((wgrad_tn_kernel<4, true, 1>), dim3(nwg), dim3(512), 0, s, g); break;
+    case 442: hipLaunchKernelGGL((wgrad_tn_kernel<4, true, 2>), dim3(nwg), dim3(512), 0, s, g); break;
+    case 443: hipLaunchKernelGGL((wgrad_tn_kernel<4, true, 3>), dim3(nwg), dim3(512), 0, s, g); break;
+    case 447: hipLaunchKernelGGL((wgrad_tn_kernel<4, true, 7>), dim3(nwg), dim3(512), 0, s, g); break;
     default: return (int)hipErrorInvalidValue;
   }
   DTD_LAUNCH_CHECK();

@@ -139,7 +139,7 @@ def test_wgrad_tn_matches_fp32(T, o, i, splits):
     assert rel(dst - 1.0, ref) < 2e-3
 
 
-@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("variant", [4, 5, 44])
 @pytest.mark.parametrize("T,o,i,splits", [(32, 256, 256, 1), (16384, 2304, 768, None), (16384, 768, 768, None),
                                           (16384, 3072, 768, None), (16384, 768, 3072, None),
                                           (4128, 512, 256, 7), (96, 256, 512, 8)])
@@ -160,7 +160,7 @@ def test_wgrad_tn_ring_matches_fp32(T, o, i, splits, variant):
     assert rel(dst - 1.0, ref) < 2e-3
 
 
-@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("variant", [4, 5, 44])
 def test_wgrad_tn_asymmetric_and_strided(variant):
     """I^T x = x exactly (a swapped accumulator map would return a transposed / permuted tile), on
     column-sliced (strided) operands."""
