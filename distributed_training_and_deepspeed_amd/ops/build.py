@@ -49,8 +49,20 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in sources() + _headers() + [Path(__file__)])
 
 
+def _file_flags(src: Path) -> list[str]:
+    """Per-source hipcc flags: a ``// hipcc-flags: ...`` line among the first 80 of the file."""
+    with open(src) as f:
+        for i, line in enumerate(f):
+            if i >= 80:
+                break
+            if line.startswith("// hipcc-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def _compile(src: Path, hipcc: str, extra: list[str]) -> Path:
     OBJ_DIR.mkdir(exist_ok=True)
+    extra = [*_file_flags(src), *extra]
     obj = OBJ_DIR / (src.stem + ".o")
     hdr_t = max((p.stat().st_mtime for p in _headers()), default=0)
     if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, hdr_t, Path(__file__).stat().st_mtime):

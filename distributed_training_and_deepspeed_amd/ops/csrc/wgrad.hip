@@ -36,6 +36,14 @@
 // MFMAs take the B fragment first (the tile is computed transposed), so a lane's accumulator holds
 // 4 consecutive columns of one row: the fp32 partial is stored as 16-byte vectors straight from
 // the accumulators.  ops/csrc/reduce.hip (splitk_reduce) sums the ranges into the gradient.
+//
+// Measured alternatives (profiles/r5_s5_wgrad_unroll.jsonl, r5_s7_wgrad_4wave.jsonl): a 5-stage
+// ring is no faster than 4; the K loop unrolled by the ring (variant 44, default) is 2-3 % faster
+// than the rolled loop; a four-wave form (one wave per SIMD, 128 x 128 per wave: a third fewer LDS
+// reads per MFMA; built with -mllvm -amdgpu-mfma-vgpr-form=1 to avoid scratch spills of its 256
+// accumulators) ran 10 % slower -- with one wave per SIMD the DMA issue and waits sit in the MFMA
+// stream.  Limiter probe (r5_s6_wgrad_limiter.jsonl, fc1 shape): no DMA -17 %, no barrier -7 %,
+// no DMA / barrier / fragment reads -37 % (2.07 PF/s, the MFMA-only loop).
 #include <type_traits>
 
 #include "common.h"
