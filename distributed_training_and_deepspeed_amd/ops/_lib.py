@@ -66,6 +66,7 @@ _SIGS = {
     "dtd_attn_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, P]),
     "dtd_attn_masks": (I, [P, I, I, I, F, P, U32, P]),
     "dtd_attn_set_bwd_form": (I, [I]),
+    "dtd_attn_fused_bwd_built": (I, []),
     # attention_f32.hip
     "dtd_attn_fwd_f32": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
     "dtd_attn_bwd_f32": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P]),
@@ -85,9 +86,6 @@ _SIGS = {
     "dtd_wgrad_tn_supported": (I, [I, I, I]),
     "dtd_wgrad_tn_splits": (I, [I, I, I]),
     "dtd_wgrad_tn": (I, [I, P, I, P, I, P, I, I, I, I, P]),
-    # gemm4.hip
-    "dtd_gemm4_supported": (I, [I, I, I]),
-    "dtd_gemm4_bt": (I, [I, P, I, P, I, P, I, P, I, I, I, P]),
     # gemm_f32.hip
     "dtd_gemm_f32_supported": (I, [I, I, I]),
     "dtd_gemm_f32_nt": (I, [P, I, P, I, P, I, P, I, I, I, P]),

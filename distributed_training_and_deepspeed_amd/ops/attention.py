@@ -118,13 +118,20 @@ def set_bwd_form(form: str) -> str:
     """'fused': one-kernel backward (one workgroup per (batch, head), dQ summed in LDS) where it
     applies -- head_dim 64, no causal mask / ALiBi, S % 128 == 0, S <= 512; 8 waves (two per SIMD)
     at S = 512, else 4.  'fused4': the 4-wave form at every S.  'split': the dQ + dK/dV
-    kernel pair.  Returns the previous form."""
+    kernel pair.  Returns the previous form.  Without an experimental build every form runs the
+    split kernels."""
     old = _lib.lib().dtd_attn_set_bwd_form(_BWD_FORMS.index(form))
     return _BWD_FORMS[old]
 
 
+def fused_bwd_built() -> bool:
+    """The one-kernel backward forms are compiled only into experimental builds
+    (DTD_BUILD_EXPERIMENTAL=1): they measured no faster than the split kernels."""
+    return _lib.has("dtd_attn_fused_bwd_built") and bool(_lib.lib().dtd_attn_fused_bwd_built())
+
+
 def fused_bwd_applies(S: int, D: int, causal: bool, slopes) -> bool:
-    return D == 64 and not causal and slopes is None and S % 128 == 0 and S <= 512
+    return D == 64 and not causal and slopes is None and S % 128 == 0 and S <= 512 and fused_bwd_built()
 
 
 def kernel_supported(qkv: torch.Tensor, D: int) -> bool:

@@ -60,9 +60,17 @@ def _file_flags(src: Path) -> list[str]:
     return []
 
 
+# DTD_BUILD_EXPERIMENTAL=1 also compiles the kernels that lost their A/B against the default path
+# (the one-kernel attention backward, the fused projection + LayerNorm GEMM); they stay opt-in at
+# run time as well.
+EXPERIMENTAL_FLAGS = ["-DDTD_ATTN_FUSED_BWD=1", "-DDTD_GEMM_LN_BUILD=1"]
+
+
 def _compile(src: Path, hipcc: str, extra: list[str]) -> Path:
     OBJ_DIR.mkdir(exist_ok=True)
     extra = [*_file_flags(src), *extra]
+    if os.environ.get("DTD_BUILD_EXPERIMENTAL") == "1":
+        extra += EXPERIMENTAL_FLAGS
     obj = OBJ_DIR / (src.stem + ".o")
     hdr_t = max((p.stat().st_mtime for p in _headers()), default=0)
     if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, hdr_t, Path(__file__).stat().st_mtime):

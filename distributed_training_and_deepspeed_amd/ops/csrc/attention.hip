@@ -37,6 +37,10 @@
 
 #include "common.h"
 
+#ifndef DTD_ATTN_FUSED_BWD
+#define DTD_ATTN_FUSED_BWD 0
+#endif
+
 using namespace dtd;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -1260,6 +1264,9 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
     }
 }
 
+#if DTD_ATTN_FUSED_BWD   // experimental builds only (DTD_BUILD_EXPERIMENTAL=1, ops/build.py): the
+                        // one-kernel backward forms measured no faster than the split kernels
+                        // (profiles/r4_attn_fused_bwd_ab.jsonl), so the default library omits them
 // ---------------------------------------------------------------------------------------------
 // Fused backward (D = 64, no causal mask, no ALiBi, S = 128 NKB <= 512): ONE workgroup per
 // (batch, head) owns every key, so dQ needs neither atomics nor a second kernel that recomputes
@@ -1792,6 +1799,8 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_fused8_kernel(BwdArgs a) {
   }
 }
 
+#endif  // DTD_ATTN_FUSED_BWD
+
 }  // namespace
 
 // Waves per SIMD the head_dim-64 kernels are compiled for (register budget 512/OCC per lane):
@@ -1906,6 +1915,8 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
 }
 
 // 0 = the dQ + dK/dV pair, 1 = fused where it applies, 2 = fused, 4-wave form; returns the previous
+DTD_EXPORT int dtd_attn_fused_bwd_built() { return DTD_ATTN_FUSED_BWD; }
+
 DTD_EXPORT int dtd_attn_set_bwd_form(int f) {
   const int old = bwd_form();
   g_bwd_form = f < 0 || f > 2 ? 0 : f;
@@ -1949,6 +1960,7 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
   BwdArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (const bf16*)o,
             (bf16*)dq, (bf16*)dk, (bf16*)dv, slopes, mA, mB, B, S, H, ld, ldo, causal, W, scale, p,
             D == 64 ? bias_part : nullptr};
+#if DTD_ATTN_FUSED_BWD
   if (D == 64 && !causal && !slopes && S % 128 == 0 && S <= 512 && bwd_fused()) {
     const bool drop = mA != nullptr;
     const dim3 g1(B * H);
@@ -1971,6 +1983,7 @@ DTD_EXPORT int dtd_attn_bwd(const void* q, const void* k, const void* v, const v
     }
     DTD_LAUNCH_CHECK();
   }
+#endif
   // dQ first: it also produces delta = rowsum(dO * O), which the dK/dV kernel then reads
   if (D == 64) {
     const int o = occupancy(2);

@@ -28,6 +28,10 @@
 #include <stdlib.h>
 #include <type_traits>
 
+// Experimental (DTD_BUILD_EXPERIMENTAL=1, ops/build.py): slower than the hipBLASLt GEMM + LayerNorm
+// kernel pair it replaces (profiles/r4_s9_results.jsonl, r5 session 9 with the asm LDS-DMA), so the
+// default library omits it and ops/gemm.py linear_ln_supported() reports it unavailable.
+#if DTD_GEMM_LN_BUILD
 #include "common.h"
 
 using namespace dtd;
@@ -458,3 +462,4 @@ DTD_EXPORT int dtd_gemm_ln(const void* x, const void* w, const void* bias, const
 #undef DTD_GLN
   DTD_LAUNCH_CHECK();
 }
+#endif  // DTD_GEMM_LN_BUILD

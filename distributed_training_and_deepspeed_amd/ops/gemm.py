@@ -270,25 +270,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
     return gemm_bt(x, w, b)
 
 
-def gemm4_supported(M: int, N: int, K: int, *tensors) -> bool:
-    """Shape / layout contract of the four-wave kernel (``ops/csrc/gemm4.hip``)."""
-    if not all(_ok(t) for t in tensors) or not _lib.has("dtd_gemm4_bt"):
-        return False
-    return bool(_lib.lib().dtd_gemm4_supported(M, N, K))
-
-
-def gemm4_bt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None,
-             out: torch.Tensor | None = None) -> torch.Tensor:
-    """a . b^T (+ bias) on the four-wave 128x128-per-wave kernel."""
-    M, K = a.shape
-    N = b.shape[0]
-    assert b.shape[1] == K
-    c = out if out is not None else torch.empty((M, N), dtype=a.dtype, device=a.device)
-    _lib.call("dtd_gemm4_bt", 0, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
-              _lib.ptr(bias), M, N, K, _lib.stream())
-    return c
-
-
 def matmul_nt(a: torch.Tensor, b_t: torch.Tensor) -> torch.Tensor:
     return gemm_bt(a, b_t)
 
@@ -486,3 +467,4 @@ def wgrad_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None, varia
     _lib.call("dtd_wgrad_tn", variant, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), part.data_ptr(), o, i,
               T, splits, _lib.stream())
     return part
+

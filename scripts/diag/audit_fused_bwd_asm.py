@@ -73,10 +73,11 @@ def audit(asm_text: str, pattern: str = KERNELS) -> list[str]:
     return problems
 
 
-def build_asm(src: str) -> str:
+def build_asm(src: str, defines=("-DDTD_ATTN_FUSED_BWD=1", "-DDTD_GEMM_LN_BUILD=1")) -> str:
+    """Device ISA of `src` (the experimental kernels compiled in: they are what is audited)."""
     out = tempfile.NamedTemporaryFile(suffix=".s", delete=False).name
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S",
-                    src, "-o", out], check=True, capture_output=True)
+                    *defines, src, "-o", out], check=True, capture_output=True)
     with open(out) as f:
         text = f.read()
     os.unlink(out)

@@ -30,7 +30,8 @@ def test_audit_flags_an_early_accumulator_read():
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc") and shutil.which("hipcc") is None,
                     reason="hipcc not available")
 def test_fused_backward_asm_mfma_results_are_waited_out():
-    text = build_asm(os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops", "csrc", "attention.hip"))
+    text = build_asm(os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops", "csrc", "attention.hip"),
+                     ["-DDTD_ATTN_FUSED_BWD=1"])
     assert "attn_bwd_fused_kernel" in text
     assert audit(text) == []
 
@@ -62,6 +63,7 @@ def test_gemm_ln_asm_mfma_results_are_waited_out():
     to AGPRs / VGPRs): every path from each MFMA -- loop back-edge, loop exit into the epilogue --
     waits its results out."""
     from audit_mfma_hazards import audit as audit_paths
-    text = build_asm(os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops", "csrc", "gemm_ln.hip"))
+    text = build_asm(os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops", "csrc", "gemm_ln.hip"),
+                     ["-DDTD_GEMM_LN_BUILD=1"])
     assert "gemm_ln_kernel" in text
     assert audit_paths(text, "gemm_ln_kernel") == []

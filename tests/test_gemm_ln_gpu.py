@@ -11,6 +11,12 @@ from distributed_training_and_deepspeed_amd.ops.rng import RngState, keep_mask
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _experimental_build():
+    if not G._lib.has("dtd_gemm_ln"):
+        pytest.skip("gemm_ln.hip is compiled only into experimental builds (DTD_BUILD_EXPERIMENTAL=1)")
+
+
 def _inputs(M, K, seed=0, bias=True):
     g = torch.Generator(device="cuda").manual_seed(seed)
     x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).bfloat16()
