@@ -30,10 +30,16 @@ import os
 
 # HIP hardware queues per process: the box default (4) is fewer than the streams of the N > 1
 # step (compute, keep-mask, optimizer, finalize and RCCL's own); streams sharing a queue
-# serialise their cross-stream waits.  Set to 8 (when unset) before anything initialises HIP
+# serialise their cross-stream waits.  Set to 8 before anything initialises HIP
 # (docs/PERFORMANCE.md, "Hardware queues").
-# A value the user set is kept as it is (e.g. 4 for an A/B run); the value in effect is logged.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# The MI355X boxes export GPU_MAX_HW_QUEUES=4 themselves, so a value below 8 is raised (with a note
+# on stderr) unless DTD_KEEP_HW_QUEUES=1 asks to keep it (A/B runs); the value in effect is logged.
+# Keeping the boxes' 4 costs the N > 1 data path 17 % (profiles/r5_s12_results.jsonl).
+_HWQ = os.environ.get("GPU_MAX_HW_QUEUES", "")
+if os.environ.get("DTD_KEEP_HW_QUEUES") != "1" and (not _HWQ.isdigit() or int(_HWQ) < 8):
+    if _HWQ:
+        print(f"[dtd] GPU_MAX_HW_QUEUES={_HWQ} raised to 8 (DTD_KEEP_HW_QUEUES=1 keeps it)", file=__import__("sys").stderr)
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 import sys
 import time
 
@@ -86,10 +92,11 @@ def parse():
                          "device or 4 MB pinned host buffer RCCL's init allocates)")
     ap.add_argument("--ddp-overlap", default="on", choices=["on", "off"],
                     help="diagnostic: off launches every bucket collective after the backward")
-    ap.add_argument("--prewarm", default="auto", choices=["auto", "none", "layer1", "tiny", "full"],
+    ap.add_argument("--prewarm", default="auto", choices=["auto", "none", "layer1", "layer1-batch", "tiny", "full"],
                     help="one forward+backward of a throwaway copy of the model before the RCCL group is "
-                         "created (auto: a 1-layer copy at batch 1 whenever a group is created; tiny: "
-                         "full depth, batch 1; full: full depth at the bench batch; utils/prewarm.py)")
+                         "created (auto: a 1-layer copy at batch 1 whenever a group is created; layer1-batch: "
+                         "1 layer at the bench batch; tiny: full depth, batch 1; full: full depth at the bench "
+                         "batch; utils/prewarm.py)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
     return ap.parse_args()
@@ -125,7 +132,7 @@ def main():
         prewarm_model_kernels(args.model, device, dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32,
                               impl=args.impl, seq_len=args.seq_len,
                               layers=None if args.prewarm in ("tiny", "full") else 1,
-                              batch=args.batch_size if args.prewarm == "full" else 1,
+                              batch=args.batch_size if args.prewarm in ("full", "layer1-batch") else 1,
                               static_mlm=not args.dense_mlm_head and args.mlm_capacity == "static",
                               **({"sparse_mlm_head": not args.dense_mlm_head} if get_config(args.model).family == "bert" else {}))
     if world > 1 or args.zero_stage is not None or args.force_collectives:   # ZeRO always runs on a group

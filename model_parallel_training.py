@@ -20,10 +20,16 @@ import os
 
 # HIP hardware queues per process: the box default (4) is fewer than the streams of the N > 1
 # step (compute, keep-mask, optimizer, finalize and RCCL's own); streams sharing a queue
-# serialise their cross-stream waits.  Set to 8 (when unset) before anything initialises HIP
+# serialise their cross-stream waits.  Set to 8 before anything initialises HIP
 # (docs/PERFORMANCE.md, "Hardware queues").
-# A value the user set is kept as it is (e.g. 4 for an A/B run); the value in effect is logged.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# The MI355X boxes export GPU_MAX_HW_QUEUES=4 themselves, so a value below 8 is raised (with a note
+# on stderr) unless DTD_KEEP_HW_QUEUES=1 asks to keep it (A/B runs); the value in effect is logged.
+# Keeping the boxes' 4 costs the N > 1 data path 17 % (profiles/r5_s12_results.jsonl).
+_HWQ = os.environ.get("GPU_MAX_HW_QUEUES", "")
+if os.environ.get("DTD_KEEP_HW_QUEUES") != "1" and (not _HWQ.isdigit() or int(_HWQ) < 8):
+    if _HWQ:
+        print(f"[dtd] GPU_MAX_HW_QUEUES={_HWQ} raised to 8 (DTD_KEEP_HW_QUEUES=1 keeps it)", file=__import__("sys").stderr)
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 import sys
 import time
 

@@ -96,6 +96,12 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "no_fused_embed_ln": _env(DTD_FUSED_EMBED_LN="0"), "no_fused_xent": _env(DTD_FUSED_XENT="0"), "fused_xent": _env(DTD_FUSED_XENT="1"), "no_defer_finalize": _env(DTD_DEFER_FINALIZE="0"),
            "gemm_stagger2": _env(DTD_GEMM_STAGGER_US="2"), "gemm_stagger4": _env(DTD_GEMM_STAGGER_US="4"),
            "attn_bwd_fused": _env(DTD_ATTN_BWD="fused"), "no_wgrad2": _env(DTD_GEMM_WGRAD="0"),
+           "fc": lambda: ["--force-collectives"],
+           "fc_prewarm_l1b": lambda: ["--force-collectives", "--prewarm", "layer1-batch"],
+           "fc_no_wgrad2": lambda: (os.environ.update(DTD_GEMM_WGRAD="0") or ["--force-collectives"]),
+           "fc_noprewarm": lambda: ["--force-collectives", "--prewarm", "none"],
+           "fc_noprewarm_eagerload": lambda: (os.environ.update(HIP_ENABLE_DEFERRED_LOADING="0")
+                                              or ["--force-collectives", "--prewarm", "none"]),
            "dmabuiltin_so": _env(DTD_KERNELS_SO=os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops",
                                                             "_dtd_kernels_dmabuiltin.so")),
            "b320": lambda: ["--batch-size", "320"], "b384": lambda: ["--batch-size", "384"],

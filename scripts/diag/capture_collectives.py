@@ -9,7 +9,7 @@ import sys
 
 CASES = ["all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor", "all_gather_coalesced", "reduce_scatter_coalesced",
          "all_gather_inplace", "reduce_scatter_inplace", "all_reduce_async_wait", "reduce_scatter_async_wait",
-         "side_stream_rs", "autograd_rs", "autograd_side_stream_rs"]
+         "side_stream_rs", "autograd_rs", "autograd_side_stream_rs", "side_stream_rs_keepwork", "side_stream_rs_evcache"]
 
 
 def child(case):
@@ -22,11 +22,19 @@ def child(case):
     xs = [torch.randn(1 << 18, device="cuda", dtype=torch.bfloat16) for _ in range(3)]
     outs = [torch.empty_like(t) for t in xs]
 
+    kept = []
+
     def side_rs():
         s2 = side[0]
         s2.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s2):
-            dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG, async_op=True).wait()
+            w = dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG, async_op=True)
+            w.wait()
+            if case == "side_stream_rs_keepwork":
+                # the Work object (and the HIP events ProcessGroupNCCL recorded for it) outlives the
+                # capture: no hipEventDestroy of a captured event before hipStreamEndCapture
+                kept.append(w)
+            del w
         torch.cuda.current_stream().wait_stream(s2)
 
     class Hook(torch.autograd.Function):      # issues the collective from the autograd thread
@@ -45,7 +53,7 @@ def child(case):
     leaf = torch.randn(4096, device="cuda", requires_grad=True)
 
     def run():
-        if case == "side_stream_rs":
+        if case in ("side_stream_rs", "side_stream_rs_keepwork", "side_stream_rs_evcache"):
             side_rs()
         elif case in ("autograd_rs", "autograd_side_stream_rs"):
             Hook.apply(leaf).sum().backward()
@@ -82,6 +90,7 @@ def child(case):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         run()
+    kept.clear()
     g.replay()
     torch.cuda.synchronize()
     print(json.dumps({"case": case, "captured_and_replayed": True}), flush=True)
@@ -94,6 +103,8 @@ def main():
         return
     for i, case in enumerate(sys.argv[1:] or CASES):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29600 + i))
+        if case == "side_stream_rs_evcache":
+            env["TORCH_NCCL_CUDA_EVENT_CACHE"] = "1"   # events returned to a cache, not destroyed
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", case], env=env,
                            capture_output=True, text=True, timeout=120)
         ok = r.returncode == 0 and "captured_and_replayed" in r.stdout
