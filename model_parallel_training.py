@@ -86,7 +86,12 @@ def main():
                         help="replay the whole step (every stage's micro-batch forwards and backwards, loss, "
                              "optimizer) as one hipGraph when all stages share one GPU; auto: on then, unless "
                              "--verbose (whose per-hook prints need eager steps)")
+    parser.add_argument("--pipe-backend", default="auto", choices=["auto", "rccl", "gloo"],
+                        help="stage-per-process mode (launched with several ranks): the point-to-point "
+                             "transport; auto = RCCL on GPUs, gloo on CPU")
     args = parser.parse_args()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return main_stage_per_process(args)
 
     config = get_config(args.model)
     dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[args.dtype]
@@ -130,7 +135,8 @@ def main():
     if args.graph == "auto":
         args.graph = "on" if one_gpu and not args.verbose else "off"
     if args.graph == "on" and not one_gpu:
-        print("--graph: stages on several devices run eagerly (one hipGraph per device is not captured)")
+        print("--graph: stages on several devices of one process run eagerly; launch one process per "
+              "stage (torchrun --nproc-per-node S) for a hipGraph per stage")
         args.graph = "off"
     batches = iter(loader)
     graphed, warm, n, loss = None, [], 0, None
@@ -182,6 +188,99 @@ def main():
                                       for d in sorted({d for d in bert.group_devices if d.type == "cuda"},
                                                       key=str)],
                       "final_loss": round(float(loss.detach()), 4) if loss is not None else None}))
+
+
+def main_stage_per_process(args):
+    """One pipeline stage per rank (``torchrun --nproc-per-node S model_parallel_training.py ...``):
+    rank s owns BertModelWithMP's s-th np.array_split module group on its own GPU, activations and
+    gradients go between ranks as RCCL send/recv (parallel/stage_pipeline.py).  Every rank issues
+    only its stage's kernels, so the step is not host-issue-bound the way one thread driving every
+    GPU is; ``--graph on`` replays each rank's whole step (sends and receives included) as one
+    hipGraph.  The idle table reports each stage's device idle time between its activities."""
+    from distributed_training_and_deepspeed_amd import comm
+    from distributed_training_and_deepspeed_amd.parallel.stage_pipeline import StagePipeline, bert_stage
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    cuda = torch.cuda.is_available()
+    backend = {"auto": "nccl" if cuda else "gloo", "rccl": "nccl", "gloo": "gloo"}[args.pipe_backend]
+    if cuda:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+    device = torch.device("cuda", torch.cuda.current_device()) if cuda else torch.device("cpu")
+    comm.init(rank=rank, world_size=world, backend=backend, local_rank=local % max(1, torch.cuda.device_count()))
+    config = get_config(args.model)
+    dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[args.dtype]
+    owner, mods = bert_stage(config, rank, world, device, dtype=dtype, impl=args.impl, seed=0)
+    chunks = args.micro_batch_count if args.pipeline else 1
+    loss_fn = Fx.CrossEntropyLoss() if args.loss == "fused" else torch.nn.CrossEntropyLoss()
+    upcast = args.loss != "fused"
+    pipe = StagePipeline(mods, rank, world, device, act_shape=lambda mb: (mb, args.seq_len, config.hidden_size),
+                         act_dtype=dtype, loss_fn=lambda out, t: loss_fn(_flat(out, upcast), t.reshape(-1)),
+                         chunks=chunks, schedule=args.schedule, set_micro=lambda m: setattr(owner.rt.rng, "micro", m))
+    optimizer = torch_adamw([p for p in pipe.parameters() if p.requires_grad], lr=5e-5)
+    dataset = load_synthetic(config, args.batch_size * args.training_steps, seq_len=args.seq_len, seed=0)
+    g = torch.Generator().manual_seed(0)
+    sampler = torch.randperm(len(dataset), generator=g).tolist()  # every rank walks the same batches
+    loader = DeviceBatchLoader(dataset, batch_size=args.batch_size, sampler=sampler, device=device)
+    pipe.train()
+
+    def step(input_ids, labels):
+        loss = pipe.train_step(input_ids if rank == 0 else None, labels if rank == world - 1 else None,
+                               rows=input_ids.shape[0])
+        optimizer.step()
+        optimizer.zero_grad()
+        owner.rt.rng.advance()
+        return loss.detach() if loss is not None else torch.zeros((), device=device)
+
+    batches = iter(loader)
+    graphed, warm, loss = None, [], None
+    if args.graph == "on" and backend != "nccl":
+        if rank == 0:
+            print("--graph: gloo stages messages through host memory (not capturable); running eagerly")
+        args.graph = "off"
+    if args.graph == "on" and cuda:
+        from distributed_training_and_deepspeed_amd.utils.graphs import CapturedStep
+        owner.tracker.enabled = False
+        warm = [b for _, b in zip(range(min(3, args.training_steps)), batches)]
+        if warm:
+            graphed = CapturedStep(step, {"input_ids": warm[0]["input_ids"], "labels": warm[0]["labels"]},
+                                   warmup_batches=[{"input_ids": b["input_ids"], "labels": b["labels"]} for b in warm])
+            loss = graphed.warmup_losses[-1]
+    comm.barrier()
+    start = time.time()
+    n = 0
+    for batch in batches:
+        if graphed is not None and batch["input_ids"].shape == graphed.static["input_ids"].shape:
+            loss = graphed(input_ids=batch["input_ids"], labels=batch["labels"])
+        else:
+            loss = step(batch["input_ids"], batch["labels"])
+        owner.step_boundary()
+        n += 1
+    if cuda:
+        torch.cuda.synchronize()
+    comm.barrier()
+    elapsed = time.time() - start
+    idle = owner.tracker.table(max(n, 1))[1 + rank][1] if graphed is None else 0.0
+    idle_all = [None] * world
+    torch.distributed.all_gather_object(idle_all, idle)
+    loss_all = [None] * world
+    torch.distributed.all_gather_object(loss_all, float(loss) if loss is not None else None)
+    if rank == 0:
+        print(f"\nTotal Training Time: {elapsed:.2f} seconds")
+        print("\nAverage Idle Time per Device:")
+        rows = [["Device", "Average Idle Time (ms)"]] + [[i, v] for i, v in enumerate(idle_all)]
+        try:
+            from tabulate import tabulate
+            print(tabulate(rows, headers="firstrow", floatfmt=".2f", tablefmt="fancy_grid"))
+        except ImportError:
+            for r in rows:
+                print(*r, sep="\t")
+        print(json.dumps({"tokens_per_s": round(n * args.batch_size * args.seq_len / max(elapsed, 1e-9), 1),
+                          "timed_steps": n, "graph": graphed is not None, "pipeline": args.pipeline,
+                          "schedule": args.schedule if args.pipeline else None, "stages": world,
+                          "mode": "stage-per-process", "transport": backend,
+                          "idle_ms_per_step": [round(v, 3) for v in idle_all],
+                          "final_loss": loss_all[-1]}))
+    comm.destroy()
 
 
 if __name__ == "__main__":
