@@ -146,7 +146,7 @@ def f32_kernel_supported(qkv: torch.Tensor, D: int) -> bool:
 
 def _masks_now(B, S, H, p, rng, sid, device) -> torch.Tensor:
     """Dropout keep bits generated on the current stream (the fp32 path)."""
-    masks = torch.empty((2, mask_words(B, H, S)), dtype=torch.int32, device=device)
+    masks = alloc_masks(B, H, S, device)
     _lib.call("dtd_attn_masks", masks.data_ptr(), B, S, H, float(p), rng.state.data_ptr(), sid, _lib.stream())
     return masks
 
@@ -165,6 +165,23 @@ def mask_words(B: int, H: int, S: int) -> int:
     """Words per keep-bit layout of one attention call: [B*H][W][32 W], W = ceil(S / 32)."""
     W = (S + 31) // 32
     return B * H * W * 32 * W
+
+
+def mask_pad_words(S: int) -> int:
+    """Slack after the second layout.  The attention kernels load keep words with unbounded scalar
+    loads: a wave whose 32 queries (keys) lie past the last word row of a tile of up to 256
+    positions still computes its row address (up to 7 rows past W), and the key blocks of the last
+    64-key tile reach up to 63 words past 32 W.  Those words are read and discarded (the scores they
+    select are masked); past the last (batch, head) plane they must still be mapped memory --
+    without the slack S = 64 read 2 rows past the end of the buffer and faulted."""
+    W = (S + 31) // 32
+    return 8 * 32 * W + 256
+
+
+def alloc_masks(B: int, H: int, S: int, device) -> torch.Tensor:
+    """[2, mask_words] int32 keep-bit buffer (both layouts back to back) with the kernels' read slack."""
+    n = mask_words(B, H, S)
+    return torch.empty(2 * n + mask_pad_words(S), dtype=torch.int32, device=device)[:2 * n].view(2, n)
 
 
 def _lm_pos(n: int) -> torch.Tensor:
@@ -209,7 +226,7 @@ def attn_masks_async(B, S, H, D, p, rng: RngState, sid, device) -> PendingMasks 
             or not _lib.has("dtd_attn_masks"):
         return None
     cur = torch.cuda.current_stream(device)
-    masks = torch.empty((2, mask_words(B, H, S)), dtype=torch.int32, device=device)
+    masks = alloc_masks(B, H, S, device)
     side = _side_stream(torch.device(device))
     side.wait_stream(cur)                      # the rng step / previous users of the buffer
     with torch.cuda.stream(side):
@@ -241,7 +258,7 @@ def attn_fwd(qkv, B, S, H, D, causal=False, slopes=None, p=0.0, rng: RngState | 
         torch.cuda.current_stream(qkv.device).wait_event(masks.event)
         masks, rng_ptr = masks.masks, None     # generated already
     elif p > 0:
-        masks = torch.empty((2, mask_words(B, H, S)), dtype=torch.int32, device=qkv.device)
+        masks = alloc_masks(B, H, S, qkv.device)
     else:
         masks = None
     sl = slopes.to(device=qkv.device, dtype=torch.float32).contiguous() if slopes is not None else None

@@ -147,12 +147,6 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __bu
 __device__ __forceinline__ f32x2 pk2(float x, float y) { return f32x2{x, y}; }
 __device__ __forceinline__ float mask_bits(float v, int m) { return __int_as_float(__float_as_int(v) & m); }
 
-__device__ __forceinline__ float keep_of(const DropoutRng& g, uint64_t e, uint32_t thr) {
-  const uint32_t b = g.bits(e >> 1);
-  const uint32_t h16 = (e & 1) ? (b >> 16) : (b & 0xffffu);
-  return h16 >= thr ? 1.f : 0.f;
-}
-
 // Keep-word layout.  Both mask layouts hold [B*H][W][Sp] words (Sp = 32 W) with the words of each
 // 32-position group permuted: the word of position 32g + c sits at 32g + lm_pos(c), c = 8a + 4b + j
 // -> 8a + 2j + b.  The words of positions c and c + 4 (b = 0) -- the two rows one accumulator
@@ -179,10 +173,6 @@ struct FwdArgs {
   float scale, p, thr;
 };
 
-// v_writelane_b32 through the LLVM intrinsic (this clang has no __builtin for it; as a real
-// intrinsic the compiler still schedules it and pads its SGPR hazards, unlike inline asm).
-extern "C" __device__ uint32_t dtd_writelane(uint32_t val, uint32_t lane, uint32_t old) __asm("llvm.amdgcn.writelane.i32");
-
 // Dropout keep-masks for one attention call, generated once in a VALU-only pass at full
 // occupancy (instead of re-hashing inside the MFMA-bound forward, dK/dV and dQ kernels) and
 // stored as bits in two layouts so every consumer reads ONE 32-bit word per 32x32 tile:
@@ -191,71 +181,55 @@ extern "C" __device__ uint32_t dtd_writelane(uint32_t val, uint32_t lane, uint32
 // Word-major ([w] outside the position) so that the 64 lanes of a consumer wave, which own 64
 // consecutive queries (keys), load one contiguous 256 B line per tile -- and the generator's
 // stores are contiguous too.
-// Random stream (ops/rng.py attn_keep_mask, bit-identical): per (bh, q, 32-key word) one
-// counter hash seeds xorshift32; output n's low / high 16 bits decide keys 2n / 2n+1.
-// grid: (ceil(S/64), B*H); block 256 = 4 waves.  Lane = query (64 per wave); each wave walks
-// key words kw = wave, wave+4, ...  Per key the keep compare is ONE v_cmp whose lane mask is
-// both the A-bit (shifted into the lane's word) and, as a ballot, the B-words of 64 queries
-// (written into lane j / 32+j with v_writelane) -- no separate transpose pass.
-__global__ void __launch_bounds__(256) attn_mask_kernel(uint32_t* __restrict__ maskA, uint32_t* __restrict__ maskB,
-                                                        int S, int W, const uint64_t* rng, uint32_t sid, uint32_t thr) {
-  DropoutRng g(rng, sid);
-  const int lane = threadIdx.x & 63, bh = blockIdx.y;
-  const int q = blockIdx.x * 64 + lane;
-  const bool qv = q < S;
-  const uint64_t ctr0 = ((uint64_t)bh * S + (uint64_t)(qv ? q : 0)) * (uint64_t)W;
-  // keep(high half) <=> x >= thr << 16 <=> x > lim; keep(low half) <=> (x << 16) > lim.  Lanes
-  // past S (and p == 1) get lim = ~0: never kept, so their ballot bits are 0 with no extra op.
-  const uint32_t lim = (qv && thr <= 0xffffu) ? (thr << 16) - 1u : 0xffffffffu;
-  const int qw = blockIdx.x * 2 + (lane >> 5);   // query word of the B entry this lane stores
-  for (int kw = threadIdx.x >> 6; kw < W; kw += 4) {
-    uint32_t x = g.bits(ctr0 + kw);
-    x = x ? x : 0x6d2b79f5u;
-    uint32_t word = 0, bw = 0;
-#pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      if (n) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; }
-      const bool c0 = (x << 16) > lim;
-      const bool c1 = x > lim;
-      word |= (c0 ? 1u : 0u) << (2 * n);
-      word |= (c1 ? 1u : 0u) << (2 * n + 1);
-      const unsigned long long b0 = __ballot(c0), b1 = __ballot(c1);
-      bw = dtd_writelane((uint32_t)b0, 2 * n, bw);
-      bw = dtd_writelane((uint32_t)(b0 >> 32), 32 + 2 * n, bw);
-      bw = dtd_writelane((uint32_t)b1, 2 * n + 1, bw);
-      bw = dtd_writelane((uint32_t)(b1 >> 32), 32 + 2 * n + 1, bw);
-    }
-    const int nk = S - kw * 32;                  // valid keys in this word
-    if (nk < 32) word &= (0xffffffffu >> (32 - nk));
-    if (qv) maskA[((size_t)bh * W + kw) * (32 * W) + lm_pos(q)] = word;
-    const int key = kw * 32 + (lane & 31);
-    if (key < S && qw < W) maskB[((size_t)bh * W + qw) * (32 * W) + lm_pos(key)] = bw;
-  }
-}
-
-// Same masks, fewer VALU issues per decision (the generator is VALU-bound: B*H*S*S decisions).
-//  * A word: d = (thr - 1) - h is negative iff keep, and v_alignbit(word, d, 31) shifts the word
-//    left by one while inserting d's sign bit -- 2 VALU per decision (the 16-bit half selected by
-//    the subtract's SDWA operand) instead of compare + select + or.  Keys enter at bit 0 in
-//    order, so one v_bfrev at the end puts key j at bit j.
-//  * B words: the 32x32 bit matrix held by each 32-lane half (row = query lane, column = key)
-//    is transposed in registers by five block-swap stages (ds_swizzle lane ^ s, v_alignbit
-//    rotate, v_bfi merge): 15 issues per word instead of 64 v_writelane.
+//
+// Random stream (ops/rng.py attn_keep_mask, bit-identical), one per (bh, query) lane:
+//  * seed: one counter hash of (bh * S + q), expanded by xorshift32 into a 16-word state s[0..15];
+//  * per 32-key word: one additive lagged-Fibonacci round with rotation,
+//      s[i] += rotl(s[(i + 11) & 15], 13)   for i = 0..15 in order (in place: lag 16 and 5),
+//    2 VALU per 32 random bits (an xorshift32 step is 6);
+//  * the 16 words are BIT PLANES: key j's 16-bit draw has bit i = bit j of s[i].  keep <=> draw
+//    >= thr is evaluated for all 32 keys at once by the LSB-first comparator
+//      acc = ~0;  acc = thr_i ? (s[i] & acc) : (s[i] | acc)     (i = 0..15)
+//    -- one v_bitop3 (majority of s[i], acc and the wave-uniform ~thr_i) per plane: 0.5 VALU per
+//    decision instead of 2-3 for extracting, comparing and inserting each 16-bit half.
+// The generator is VALU-bound (B*H*S*S decisions per layer): ~80 VALU per 32-key word against
+// ~230 for the round-2..4 form (hash-seeded xorshift per word, alignbit sign insertion).
+// B words: the 32x32 bit matrix held by each 32-lane half (row = query lane, column = key) is
+// transposed in registers by five block-swap stages (ds_swizzle lane ^ s, v_alignbit rotate,
+// v_bfi merge): 15 issues per word.
+// grid: (ceil(S / 256), B*H); block 256 = 4 waves of 64 consecutive queries, each walking all W
+// key words of its queries (the stream is sequential in the word index).
 template <int S_>
 __device__ __forceinline__ uint32_t swap_stage(uint32_t t, uint32_t sh, uint32_t mk) {
   const uint32_t y = (uint32_t)__builtin_amdgcn_ds_swizzle((int)t, (S_ << 10) | 0x1f);   // lane ^ S_ (32-lane groups)
   const uint32_t rot = __builtin_amdgcn_alignbit(y, y, sh);
   return (rot & mk) | (t & ~mk);
 }
-__global__ void __launch_bounds__(256) attn_mask_kernel_t(uint32_t* __restrict__ maskA, uint32_t* __restrict__ maskB,
-                                                          int S, int W, const uint64_t* rng, uint32_t sid, uint32_t thr) {
-  DropoutRng g(rng, sid);
+constexpr int kMaskRot = 13;     // rotl amount of the lagged-Fibonacci round
+__global__ void __launch_bounds__(256) attn_mask_kernel(uint32_t* __restrict__ maskA, uint32_t* __restrict__ maskB,
+                                                        int S, int W, const uint64_t* rng, uint32_t sid, uint32_t thr) {
   const int lane = threadIdx.x & 63, bh = blockIdx.y;
-  const int q = blockIdx.x * 64 + lane;
+  const int q0 = blockIdx.x * 256 + (threadIdx.x & ~63);     // first query of this wave
+  if (q0 >= 32 * W) return;                                   // wave-uniform: nothing to store
+  DropoutRng g(rng, sid);
+  const int q = q0 + lane;
   const bool qv = q < S;
-  const uint64_t ctr0 = ((uint64_t)bh * S + (uint64_t)(qv ? q : 0)) * (uint64_t)W;
-  // keep <=> h >= thr <=> (thr - 1) - h < 0; lanes past S never keep (h <= 65535)
-  const int thm1 = qv ? (int)thr - 1 : 65535;
+  uint32_t st[16];
+  {
+    uint32_t x = g.bits((uint64_t)bh * S + (uint64_t)(qv ? q : 0));
+    x = x ? x : 0x6d2b79f5u;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; }
+      st[i] = x;
+    }
+  }
+  // comparator constants: nt[i] = ~0 where thr's bit i is 0 (OR), 0 where it is 1 (AND); p = 1
+  // (thr = 65536) and lanes past S keep nothing
+  uint32_t nt[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) nt[i] = ((thr >> i) & 1u) ? 0u : 0xffffffffu;
+  const uint32_t live = (qv && thr < 65536u) ? 0xffffffffu : 0u;
   // per-stage lane constants of the transpose: rotate amount and merge mask
   uint32_t sh[5], mk[5];
 #pragma unroll
@@ -266,21 +240,19 @@ __global__ void __launch_bounds__(256) attn_mask_kernel_t(uint32_t* __restrict__
     sh[i] = up ? s : 32 - s;
     mk[i] = up ? ~Hs : Hs;
   }
-  const int qw = blockIdx.x * 2 + (lane >> 5);   // query word of the B entry this lane stores
-  for (int kw = threadIdx.x >> 6; kw < W; kw += 4) {
-    uint32_t x = g.bits(ctr0 + kw);
-    x = x ? x : 0x6d2b79f5u;
-    uint32_t word = 0;
+  const int qw = q0 / 32 + (lane >> 5);          // query word of the B entry this lane stores
+  uint32_t* pa = maskA + (size_t)bh * W * (32 * W) + lm_pos(q);
+  for (int kw = 0; kw < W; ++kw) {
+    uint32_t acc = 0xffffffffu;
 #pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      if (n) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; }
-      word = __builtin_amdgcn_alignbit(word, (uint32_t)(thm1 - (int)(x & 0xffffu)), 31);
-      word = __builtin_amdgcn_alignbit(word, (uint32_t)(thm1 - (int)(x >> 16)), 31);
+    for (int i = 0; i < 16; ++i) {
+      st[i] += __builtin_amdgcn_alignbit(st[(i + 11) & 15], st[(i + 11) & 15], 32 - kMaskRot);
+      acc = __builtin_amdgcn_bitop3_b32(st[i], acc, nt[i], 0xe8);   // majority(s, acc, nt)
     }
-    word = __builtin_bitreverse32(word);
+    uint32_t word = acc & live;
     const int nk = S - kw * 32;                  // valid keys in this word
     if (nk < 32) word &= (0xffffffffu >> (32 - nk));
-    if (qv) maskA[((size_t)bh * W + kw) * (32 * W) + lm_pos(q)] = word;
+    if (qv) pa[(size_t)kw * (32 * W)] = word;
     uint32_t t = word;
     t = swap_stage<16>(t, sh[0], mk[0]);
     t = swap_stage<8>(t, sh[1], mk[1]);
@@ -290,11 +262,6 @@ __global__ void __launch_bounds__(256) attn_mask_kernel_t(uint32_t* __restrict__
     const int key = kw * 32 + (lane & 31);
     if (key < S && qw < W) maskB[((size_t)bh * W + qw) * (32 * W) + lm_pos(key)] = t;
   }
-}
-
-static bool mask_ballot() {
-  static const int v = [] { const char* e = getenv("DTD_ATTN_MASK"); return e && e[0] == '0' ? 1 : 0; }();
-  return v != 0;
 }
 
 // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs, each with its own
@@ -1887,8 +1854,8 @@ DTD_EXPORT int dtd_attn_fwd(const void* q, const void* k, const void* v, void* o
     // stream, overlapping the QKV GEMM)
     if (rng) {
       uint32_t* mB = masks + (size_t)B * H * (32 * W) * W;
-      hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : attn_mask_kernel_t, dim3((S + 63) / 64, B * H), dim3(256), 0,
-                         s, mA, mB, S, W, rng, sid, keep_threshold(p));
+      hipLaunchKernelGGL(attn_mask_kernel, dim3((S + 255) / 256, B * H), dim3(256), 0, s, mA, mB, S, W, rng, sid,
+                         keep_threshold(p));
     }
   }
   const char* thr_env = getenv("DTD_ATTN_RESCALE_THR");
@@ -1930,8 +1897,8 @@ DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, con
   if (B * S * H == 0 || p <= 0.f) return 0;
   if (!masks || !rng) return (int)hipErrorInvalidValue;
   const int W = (S + 31) / 32;
-  hipLaunchKernelGGL(mask_ballot() ? attn_mask_kernel : attn_mask_kernel_t, dim3((S + 63) / 64, B * H), dim3(256), 0, s,
-                     masks, masks + (size_t)B * H * (32 * W) * W, S, W, rng, sid, keep_threshold(p));
+  hipLaunchKernelGGL(attn_mask_kernel, dim3((S + 255) / 256, B * H), dim3(256), 0, s, masks,
+                     masks + (size_t)B * H * (32 * W) * W, S, W, rng, sid, keep_threshold(p));
   DTD_LAUNCH_CHECK();
 }
 

@@ -75,30 +75,42 @@ def _xorshift32(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def _rotl32(x: torch.Tensor, r: int) -> torch.Tensor:
+    return ((x << r) & M32) | (x >> (32 - r))
+
+
+ATTN_MASK_ROT = 13   # ops/csrc/attention.hip kMaskRot
+
+
 def attn_keep_mask(B: int, H: int, S: int, p: float, seed: int, step: int, sid: int, device="cpu") -> torch.Tensor:
     """Bool keep-mask [B, H, S, S] of attention-probability dropout (identical to the HIP mask
     generator, ops/csrc/attention.hip ``attn_mask_kernel``).
 
-    Per (batch*head, query, 32-key word) one counter hash seeds an xorshift32 stream; its 16
-    outputs give the 32 keep decisions of the word (low / high 16 bits of output n -> keys
-    2n / 2n+1, keep iff >= the 16-bit threshold).  B*H*S*S decisions per layer make the
-    generator VALU-bound, so only one of every 16 32-bit draws pays for the full (two-multiply)
-    mix; the rest are three shift-xor pairs."""
+    One stream per (batch*head, query): a counter hash of (bh * S + q) expanded by xorshift32 into
+    a 16-word state; per 32-key word one additive lagged-Fibonacci round with rotation
+    (``s[i] += rotl(s[(i + 11) & 15], 13)``, i ascending, in place).  The 16 words are bit planes:
+    key j's 16-bit draw has bit i = bit j of s[i], and keep iff draw >= the 16-bit threshold --
+    evaluated for all 32 keys at once by an LSB-first bitwise comparator (the GPU form spends one
+    majority op per plane; B*H*S*S decisions per layer make the generator VALU-bound)."""
     k0, k1 = _keys(seed, step, sid)
     W = (S + 31) // 32
-    ctr = torch.arange(B * H * S * W, dtype=torch.int64, device=device)
+    ctr = torch.arange(B * H * S, dtype=torch.int64, device=device)
     lo, hi = ctr & M32, ctr >> 32
     x = _mix32(((lo ^ k0) + (((hi * 0xC2B2AE35) & M32) ^ k1)) & M32)
     x = torch.where(x == 0, torch.full_like(x, 0x6D2B79F5), x)
+    st = [x]
+    for _ in range(15):
+        st.append(_xorshift32(st[-1]))
     thr = keep_threshold(p)
-    outs = []
-    for n in range(16):
-        if n:
-            x = _xorshift32(x)
-        outs.append((x & 0xFFFF) >= thr)
-        outs.append((x >> 16) >= thr)
-    keep = torch.stack(outs, -1).view(B, H, S, W * 32)
-    return keep[..., :S].contiguous()
+    words = []
+    for _ in range(W):
+        acc = torch.full_like(x, M32)
+        for i in range(16):
+            st[i] = (st[i] + _rotl32(st[(i + 11) & 15], ATTN_MASK_ROT)) & M32
+            acc = (st[i] & acc) if (thr >> i) & 1 else (st[i] | acc)
+        words.append(acc if thr < 65536 else torch.zeros_like(acc))
+    bits = (torch.stack(words, -1).unsqueeze(-1) >> torch.arange(32, dtype=torch.int64, device=device)) & 1
+    return bits.view(B, H, S, W * 32)[..., :S].bool().contiguous()
 
 
 class RngState:

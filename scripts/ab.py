@@ -108,7 +108,11 @@ PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned
            "dkdv_occ1": _env(DTD_ATTN_OCC="3,1,3"),
            "gemm_ln": _env(DTD_GEMM_LN="1"), "gemm_ln_p0": _env(DTD_GEMM_LN="1", DTD_GEMM_LN_PIPE="0"),
            "base_so": _env(DTD_KERNELS_SO=os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops",
-                                                      "_dtd_kernels_base.so"))}
+                                                      "_dtd_kernels_base.so")),
+           # round-4 keep-mask generator (per-word xorshift + alignbit insertion), built from the
+           # previous attention.hip into ops/_dtd_kernels_oldmask.so
+           "oldmask_so": _env(DTD_KERNELS_SO=os.path.join(ROOT, "distributed_training_and_deepspeed_amd", "ops",
+                                                         "_dtd_kernels_oldmask.so"))}
 
 
 def child(variant, bench_args):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Attention-dropout keep-bit generator (attention.hip) at the bench shape (b256 x 12 heads x
-S 512): microseconds per call and a checksum of both mask layouts (so the transpose generator
-and the ballot generator, DTD_ATTN_MASK=0, can be compared bit for bit across processes)."""
+S 512): microseconds per call and a checksum of both mask layouts.  DTD_KERNELS_SO=<library>
+times another build of the generator (e.g. ops/_dtd_kernels_oldmask.so, the round-4 form)."""
 import json
 import os
 import sys
@@ -18,7 +18,7 @@ def main():
     B, H, S, p = int(os.environ.get("B", 256)), 12, int(os.environ.get("S", 512)), 0.1
     W = (S + 31) // 32
     rg = RngState(5, device="cuda")
-    masks = torch.empty((2, A.mask_words(B, H, S)), dtype=torch.int32, device="cuda")
+    masks = A.alloc_masks(B, H, S, "cuda")
     st = torch.cuda.current_stream().cuda_stream
 
     def run():
@@ -39,7 +39,7 @@ def main():
         ts.append(e0.elapsed_time(e1) / 20 * 1e3)
     ts.sort()
     dec = B * H * S * S
-    print(json.dumps({"variant": "ballot" if os.environ.get("DTD_ATTN_MASK") == "0" else "transpose",
+    print(json.dumps({"variant": os.path.basename(os.environ.get("DTD_KERNELS_SO", "default")),
                       "B": B, "S": S, "us": round(ts[2], 1), "Gdecisions_per_s": round(dec / ts[2] / 1e3, 1),
                       "checksum": chk}), flush=True)
 

@@ -27,6 +27,7 @@ CASES = [
     (1, 200, 2, 64, True, True, 0.1),
     (1, 256, 2, 128, False, False, 0.0),
     (1, 160, 2, 128, True, False, 0.1),
+    (2, 64, 2, 64, False, False, 0.1),     # S < one 128-query tile: mask rows past W are over-read
 ]
 
 
