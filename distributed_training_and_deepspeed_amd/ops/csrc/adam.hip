@@ -26,8 +26,13 @@ struct AdamArgs {
   float* p; float* m; float* v; const void* g; bf16* p_lp; size_t n; const float* hp; int mode; int g_dtype;
 };
 
+// Contraction off: the same element must round identically in the 8-wide body and in the scalar
+// tail (a staged update launches per stage span, so an element can be a tail element in one launch
+// and a vector element in the whole-buffer launch; with the compiler free to fuse multiply-adds
+// differently in the two contexts the results differed in the last bit -- r5 s19).
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float lr, float b1, float b2,
                                           float eps, float wd, float bc1, float bc2_sqrt, int mode) {
+#pragma clang fp contract(off)
   if (!(mode & 1) && wd != 0.f) g += wd * p;
   m = b1 * m + (1.f - b1) * g;
   v = b2 * v + (1.f - b2) * g * g;
