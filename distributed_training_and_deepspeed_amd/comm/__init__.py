@@ -102,6 +102,8 @@ def destroy(barrier: bool | None = None) -> None:
         if barrier:
             dist.barrier()
     finally:
+        from ..utils.graphs import release_group_graphs
+        release_group_graphs()   # graphs holding this group's RCCL work go before the communicator
         dist.destroy_process_group()
 
 

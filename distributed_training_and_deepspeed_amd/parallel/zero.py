@@ -152,6 +152,32 @@ def _split_buckets(params, cap_elems: int):
     return buckets
 
 
+class _WorkFence:
+    """A collective still in flight, used where the eager path records a HIP event on the comm
+    stream: a landing region's release fence, a ZeRO-3 unit's gather fence.  Inside a hipGraph
+    capture the collectives are issued on the capturing stream (a collective issued on a side
+    stream forked from the capture crashes hipStreamEndCapture: RCCL's internal stream then forks
+    from a non-origin stream -- scripts/diag/capture_collectives.py, profiles/r5_capture_results.jsonl)
+    and their ``Work.wait()`` -- the capturing stream waiting for the collective's end -- is
+    deferred to the first reader of the bytes: in the graph each collective is a branch parallel
+    to the backward / forward work issued after it."""
+
+    __slots__ = ("work",)
+
+    def __init__(self, work):
+        self.work = work
+
+
+def _fence_wait(fence, stream=None) -> None:
+    """Make the current stream (``stream``) wait for a HIP event or a pending collective."""
+    if fence is None:
+        return
+    if isinstance(fence, _WorkFence):
+        fence.work.wait()           # ProcessGroupNCCL: the current stream waits for the end event
+    else:
+        (stream or torch.cuda.current_stream()).wait_event(fence)
+
+
 class _Arena:
     """Ring sub-allocator over ONE persistent buffer (ZeRO-2/3 gradient landing regions and
     ZeRO-3 gathered-parameter regions).
@@ -220,6 +246,16 @@ class _Arena:
         self.head = a + n
         return self.buf[a:a + n]
 
+    def drop_work_fences(self) -> None:
+        """Forget the pending-collective fences (a captured step joined them all on the capturing
+        stream, so later acquirers on that stream are already ordered behind them); no RCCL Work
+        object may outlive the capture that created it (one freed after its process group is
+        destroyed crashed the next test's replay)."""
+        self.done = [(a, b, None if isinstance(ev, _WorkFence) else ev) for a, b, ev in self.done]
+        for d in self.dedicated.values():
+            if isinstance(d[1], _WorkFence):
+                d[1] = None
+
     def release(self, t: torch.Tensor, event=None, stream=None) -> None:
         for d in self.dedicated.values():
             if d[0].data_ptr() == t.data_ptr() and d[2]:
@@ -287,6 +323,9 @@ class ZeroEngine(nn.Module):
         self._callback_queued = False
         self._need_reset = True
         self._refresh_events = {}   # segment index -> event of its last refresh all-gather
+        self._cap_pending = []      # _WorkFence of collectives issued inside a capture, not yet joined
+        # DTD_ZERO_CAPTURE_DEFER=0: inside a capture every collective is waited where it is issued
+        self._defer_capture = os.environ.get("DTD_ZERO_CAPTURE_DEFER", "1") == "1"
         self._refresh_waits = {}    # id(module) -> segment indices its forward reads
 
         # ---- partition parameters into persistent buckets and (stage 3) units
@@ -560,7 +599,8 @@ class ZeroEngine(nn.Module):
                 p._dtd_touched = False
             return
         cur = torch.cuda.current_stream(self.device) if self.cuda else None
-        s.gbuf = self.landing.acquire(s.numel, s.index, waiter=cur.wait_event if cur is not None else None)
+        s.gbuf = self.landing.acquire(s.numel, s.index,
+                                      waiter=(lambda f: _fence_wait(f, cur)) if cur is not None else None)
         # padding (alignment gaps, segment tail) must reduce as zeros: the region is recycled.  Only
         # the padding is cleared (one index_fill_ launch): every parameter's own range is written
         # in full by its first contribution (grad_dst: accumulate=False) or zeroed in
@@ -634,12 +674,20 @@ class ZeroEngine(nn.Module):
         # stages 2/3 reduce every micro-batch and accumulate the shards
         first = self.micro_step == 0 or self.stage <= 1 or self.replicated
         out = self.gshard[s.shard_off:s.shard_off + s.chunk]
+        # inside a capture an RCCL collective is left in flight (its wait deferred to the readers:
+        # the landing region's next acquirer, the end of the backward); what reads the result right
+        # away (gloo's division, the accumulation add) waits here
+        defer = self._defer_capture and self._capturing() and self.backend == "nccl"
+        fence = None
         with self._comm_ctx():
             if self.replicated:  # buf aliases the gradient "shard" (the full buffer)
                 if self.collect:
                     op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
                     w = clog.all_reduce(buf, op=op, group=self.group, async_op=True)
-                    w.wait()
+                    if defer:
+                        fence = _WorkFence(w)
+                    else:
+                        w.wait()
                     if self.backend != "nccl":
                         buf.div_(self.world)
             else:
@@ -647,7 +695,10 @@ class ZeroEngine(nn.Module):
                 if self.collect:
                     op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
                     w = clog.reduce_scatter_tensor(dst, buf, op=op, group=self.group, async_op=True)
-                    w.wait()
+                    if defer and first:
+                        fence = _WorkFence(w)
+                    else:
+                        w.wait()
                     if self.backend != "nccl":
                         dst.div_(self.world)
                 elif dst.data_ptr() != buf.data_ptr():   # aliased stage-3 unit: already in place
@@ -657,7 +708,10 @@ class ZeroEngine(nn.Module):
             ev = None
             landed = (self.stage >= 2 and not self.replicated) or s.unit
             cs = self._cs()
-            if cs is not None and landed:
+            if fence is not None:
+                self._cap_pending.append(fence)
+                ev = fence
+            elif cs is not None and landed:
                 ev = torch.cuda.Event()
                 ev.record(cs)
         if landed:
@@ -683,8 +737,21 @@ class ZeroEngine(nn.Module):
             if not s.launched:
                 self._reduce_unit(s)
         self._release_pending()
+        self._join_captured()
         if self._cs() is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+
+    def _join_captured(self) -> None:
+        """Join every collective a capture left in flight (the optimizer reads the shards next)."""
+        if not self._cap_pending:
+            return
+        for f in self._cap_pending:
+            f.work.wait()
+        self._cap_pending.clear()
+        self.landing.drop_work_fences()
+        for u in self.units:
+            if isinstance(u.gather_event, _WorkFence):
+                u.gather_event = None
 
     # ================================================================== stage 3 units
     def _install_unit_hooks(self) -> None:
@@ -705,7 +772,11 @@ class ZeroEngine(nn.Module):
         with self._comm_ctx(self.gather_stream):   # the stream wait orders it behind earlier reads
             if self.collect:
                 w = clog.all_gather_into_tensor(full, src, group=self.gather_group, async_op=True)
-                w.wait()
+                if self._defer_capture and self._capturing() and self.backend == "nccl":
+                    s.gather_event = _WorkFence(w)     # waited by the unit's first reader (_ensure)
+                    self._cap_pending.append(s.gather_event)
+                else:
+                    w.wait()
             else:
                 full.copy_(src)
             if self.gather_stream is not None and not self._capturing():
@@ -719,14 +790,14 @@ class ZeroEngine(nn.Module):
     def _ensure(self, s: _Segment) -> None:
         self._gather(s)
         if s.gather_event is not None:
-            torch.cuda.current_stream(self.device).wait_event(s.gather_event)
+            _fence_wait(s.gather_event, torch.cuda.current_stream(self.device))
             s.gather_event = None
 
     def _release(self, s: _Segment) -> None:
         if s.full is None:
             return
         if s.gather_event is not None:   # gathered (prefetched) but never used: still order it
-            torch.cuda.current_stream(self.device).wait_event(s.gather_event)
+            _fence_wait(s.gather_event, torch.cuda.current_stream(self.device))
             s.gather_event = None
         if not self.alias_units:
             if self.config.poison_released and s.full.is_floating_point():
@@ -848,6 +919,7 @@ class ZeroEngine(nn.Module):
             self.micro_step += 1
             self._need_reset = True
             return
+        self._join_captured()
         if self._cs() is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
         self.optimizer.step()

@@ -18,15 +18,35 @@ What makes the step capturable (and is kept that way by the framework):
 """
 from __future__ import annotations
 
+import gc
 import math
+import time
+import weakref
 
 import torch
+
+# captured steps recorded while a process group existed (their graphs may hold RCCL work)
+_WITH_GROUP: "weakref.WeakSet[CapturedStep]" = weakref.WeakSet()
 
 
 def mlm_capacity(tokens: int, p: float = 0.15, sigmas: float = 8.0) -> int:
     """Static labelled-row capacity: mean + 8 sigma of Binomial(tokens, p) (+64), capped."""
     mean, sd = tokens * p, math.sqrt(tokens * p * (1 - p))
     return min(tokens, int(math.ceil(mean + sigmas * sd)) + 64)
+
+
+# ProcessGroupNCCL's watchdog thread polls the end events of enqueued collectives every 100 ms; one
+# that polls a warm-up collective while a (global-mode) capture runs gets "operation not permitted
+# when stream is capturing" and aborts the process (profiles/r5_capture_results.jsonl).  Collectives
+# issued during a capture are not enqueued to it, so once it has retired the (completed) warm-up
+# work it makes no HIP call until the capture ends.
+_WATCHDOG_DRAIN_S = 0.35
+
+
+def _drain_rccl_watchdog() -> None:
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        time.sleep(_WATCHDOG_DRAIN_S)
 
 
 class CapturedStep:
@@ -51,12 +71,27 @@ class CapturedStep:
                 self.warmup_losses.append(step_fn(**b))
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        _drain_rccl_watchdog()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = step_fn(**self.static)
         self.warmup = len(batches)
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            _WITH_GROUP.add(self)
+
+    def release(self) -> None:
+        """Destroy the graph (and its memory pool) now rather than whenever the garbage collector
+        reaches this object."""
+        if self.graph is not None:
+            torch.cuda.synchronize()
+            self.graph.reset()
+        self.graph, self.out = None, None
 
     def __call__(self, **inputs):
+        if self.graph is None:
+            raise RuntimeError("CapturedStep: the graph was released (comm.destroy() releases the graphs "
+                               "captured with its process group)")
         for k, v in inputs.items():
             self.static[k].copy_(v, non_blocking=True)
         self.graph.replay()
@@ -65,3 +100,14 @@ class CapturedStep:
     def check(self) -> None:
         if self.rt is not None and self.rt.mlm_overflow is not None and bool(self.rt.mlm_overflow):
             raise RuntimeError("a batch had more labelled rows than rt.mlm_capacity: raise the capacity")
+
+
+def release_group_graphs() -> None:
+    """Reset every live captured step recorded while a process group existed.  ``comm.destroy()``
+    calls this before destroying the group, so a hipGraph holding RCCL collectives never outlives
+    its communicator (a step object kept alive by a reference cycle would otherwise be destroyed at
+    some later garbage collection, after the communicator is gone)."""
+    gc.collect()
+    for cs in list(_WITH_GROUP):
+        cs.release()
+    _WITH_GROUP.clear()

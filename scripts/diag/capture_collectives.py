@@ -9,7 +9,8 @@ import sys
 
 CASES = ["all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor", "all_gather_coalesced", "reduce_scatter_coalesced",
          "all_gather_inplace", "reduce_scatter_inplace", "all_reduce_async_wait", "reduce_scatter_async_wait",
-         "side_stream_rs", "autograd_rs", "autograd_side_stream_rs", "side_stream_rs_keepwork", "side_stream_rs_evcache"]
+         "side_stream_rs", "autograd_rs", "autograd_side_stream_rs", "side_stream_rs_keepwork", "side_stream_rs_evcache",
+         "side_stream_rs_join_origin", "side_stream_rs_origin_only", "origin_deferred_wait"]
 
 
 def child(case):
@@ -29,13 +30,18 @@ def child(case):
         s2.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s2):
             w = dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG, async_op=True)
-            w.wait()
+            if case != "side_stream_rs_origin_only":
+                w.wait()
             if case == "side_stream_rs_keepwork":
                 # the Work object (and the HIP events ProcessGroupNCCL recorded for it) outlives the
                 # capture: no hipEventDestroy of a captured event before hipStreamEndCapture
                 kept.append(w)
-            del w
         torch.cuda.current_stream().wait_stream(s2)
+        if case in ("side_stream_rs_join_origin", "side_stream_rs_origin_only"):
+            # RCCL's internal stream forked from s2: join it into the ORIGIN (capturing) stream
+            # directly -- the Work's end event waited on the origin stream
+            w.wait()
+        del w
 
     class Hook(torch.autograd.Function):      # issues the collective from the autograd thread
         @staticmethod
@@ -53,10 +59,18 @@ def child(case):
     leaf = torch.randn(4096, device="cuda", requires_grad=True)
 
     def run():
-        if case in ("side_stream_rs", "side_stream_rs_keepwork", "side_stream_rs_evcache"):
+        if case.startswith("side_stream_rs"):
             side_rs()
         elif case in ("autograd_rs", "autograd_side_stream_rs"):
             Hook.apply(leaf).sum().backward()
+        elif case == "origin_deferred_wait":
+            # issued on the capturing stream, waited only after unrelated work on that stream: in the
+            # graph the collective is a branch parallel to that work (ZeRO's captured-step form)
+            w = dist.reduce_scatter_tensor(out, x, op=dist.ReduceOp.AVG, async_op=True)
+            for _ in range(4):
+                leaf.data.mul_(1.0001)
+            w.wait()
+            out.add_(1.0)
         elif case == "all_reduce":
             dist.all_reduce(x, op=dist.ReduceOp.AVG)
         elif case == "reduce_scatter_tensor":
@@ -91,6 +105,14 @@ def child(case):
     with torch.cuda.graph(g):
         run()
     kept.clear()
+    if case == "origin_deferred_wait":
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        want = x.float() + 1.0          # world 1: the reduce-scatter output is the input
+        if not torch.allclose(out.float(), want, atol=5e-2):
+            print(json.dumps({"case": case, "mismatch": (out.float() - want).abs().max().item()}), flush=True)
+            sys.exit(1)
     g.replay()
     torch.cuda.synchronize()
     print(json.dumps({"case": case, "captured_and_replayed": True}), flush=True)
