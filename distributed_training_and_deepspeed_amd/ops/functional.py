@@ -114,14 +114,15 @@ def _finalize_stream(part: torch.Tensor, defer: bool = True) -> int:
     """Stream for a column-sum finalize of gradient partials.  Inside a DDP backward window
     (``grad.defer_finalize``) the ~10 us finalize launches go to the async-gradient side stream,
     off the dgrad chain: the side stream waits for the partials' producer, the partial buffer is
-    recorded on it, and the reducer joins it before any collective or the optimizer reads a
+    held until the join, and the reducer joins it before any collective or the optimizer reads a
     gradient (``join_async_wgrad``)."""
     from .grad import finalize_side_stream
     side = finalize_side_stream(part.device) if defer and part.is_cuda else None
     if side is None:
         return _lib.stream()
     side.wait_stream(torch.cuda.current_stream(part.device))
-    part.record_stream(side)
+    from .grad import hold_until_join
+    hold_until_join(part)   # freed after the reducer's join (not record_stream: ops/grad.py emit_wgrad)
     return side.cuda_stream
 
 

@@ -74,7 +74,7 @@ def _env(**kv):
     return f
 
 
-PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned, "mlm_static": _mlm_static, "mlm_dynamic": lambda: ["--mlm-capacity", "dynamic"], "graph": lambda: ["--graph", "on"],
+PATCHES = {"async_wgrad": lambda: ["--async-wgrad", "on"], "no_tuned": _no_tuned, "mlm_static": _mlm_static, "mlm_dynamic": lambda: ["--mlm-capacity", "dynamic"], "graph": lambda: ["--graph", "on"], "graph_async_wgrad": lambda: ["--graph", "on", "--async-wgrad", "on"],
            "attn_occ_323": _env(DTD_ATTN_OCC="3,2,3"), "attn_occ_222_dq64": _env(DTD_ATTN_TILE="64,64"),
            "attn_occ_322": _env(DTD_ATTN_OCC="3,2,2"), "attn_occ_323_dq64": _env(DTD_ATTN_OCC="3,2,3", DTD_ATTN_TILE="64,64"),
            "wgrad_s1": _wgrad_fixed(1), "wgrad_s4": _wgrad_fixed(4), "wgrad_s8": _wgrad_fixed(8),
