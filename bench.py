@@ -135,8 +135,17 @@ def main():
                               batch=args.batch_size if args.prewarm in ("full", "layer1-batch") else 1,
                               static_mlm=not args.dense_mlm_head and args.mlm_capacity == "static",
                               **({"sparse_mlm_head": not args.dense_mlm_head} if get_config(args.model).family == "bert" else {}))
+    probe = None
+    if cuda and (world > 1 or args.zero_stage is not None or args.force_collectives):
+        from distributed_training_and_deepspeed_amd.utils.prewarm import KernelProbe
+        probe = KernelProbe(device)   # probe kernel 0 runs before the communicator exists
     if world > 1 or args.zero_stage is not None or args.force_collectives:   # ZeRO always runs on a group
         comm.init(rank=rank, world_size=world, local_rank=local)
+    post_init = probe.measure() if probe is not None else None
+    if post_init is not None and post_init["ratio"] > 1.05:
+        print(f"[dtd] WARNING: a kernel first launched after comm.init runs {post_init['ratio']:.3f}x slower "
+              "than its twin launched before it: kernels the prewarm did not cover may be slow in this "
+              "process (utils/prewarm.py, ops/csrc/probe.hip)", file=sys.stderr)
     elif args.comm_init != "none":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29561")
@@ -302,6 +311,7 @@ def main():
                 "tuned_gemms": tuned,
                 "hip_graph": graphed is not None,
                 "force_collectives": args.force_collectives,
+                "post_init_kernel_probe": post_init,
                 "async_wgrad": args.async_wgrad == "on",
                 "opt_overlap": opt_overlap,
                 "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if cuda else None,
