@@ -468,3 +468,4 @@ def wgrad_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None, varia
               T, splits, _lib.stream())
     return part
 
+
