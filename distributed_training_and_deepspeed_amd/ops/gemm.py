@@ -467,5 +467,3 @@ def wgrad_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None, varia
     _lib.call("dtd_wgrad_tn", variant, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), part.data_ptr(), o, i,
               T, splits, _lib.stream())
     return part
-
-
