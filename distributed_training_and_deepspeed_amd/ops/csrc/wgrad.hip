@@ -312,9 +312,11 @@ DTD_EXPORT int dtd_wgrad_tn(int variant, const void* a, int lda, const void* b, 
                             int K, int splits, hipStream_t s) {
   if (!dtd_wgrad_tn_supported(M, N, K) || splits < 1) return (int)hipErrorInvalidValue;
   if ((lda | ldb) % 8 || lda < M || ldb < N) return (int)hipErrorInvalidValue;
-  if ((size_t)K * lda * 2 >= 0x7fffffffull || (size_t)K * ldb * 2 >= 0x7fffffffull) return (int)hipErrorInvalidValue;
   const int nk = K / BK;
   const int ksplit = (nk + splits - 1) / splits;
+  // buffer offsets are 32-bit; each workgroup's resource starts at its own K-range
+  const size_t rows = (size_t)ksplit * BK;
+  if (rows * lda * 2 >= 0x7fffffffull || rows * ldb * 2 >= 0x7fffffffull) return (int)hipErrorInvalidValue;
   WgArgs g{(const bf16*)a, (const bf16*)b, (float*)part, M, N, K, lda, ldb, splits, ksplit};
   const int nwg = (M / BM) * (N / BN) * splits;
   if (variant == 0) variant = 44;   // 128 KiB: leaves LDS for a co-resident side-stream kernel

@@ -453,7 +453,13 @@ def wgrad_supported(dy: torch.Tensor, x: torch.Tensor) -> bool:
     row-major views on the GPU, o and i multiples of 256, T a multiple of 32."""
     if not (_ok(dy) and _ok(x)) or dy.shape[0] != x.shape[0] or not _lib.has("dtd_wgrad_tn"):
         return False
-    return bool(_lib.lib().dtd_wgrad_tn_supported(dy.shape[1], x.shape[1], dy.shape[0]))
+    T, o, i = dy.shape[0], dy.shape[1], x.shape[1]
+    if not _lib.lib().dtd_wgrad_tn_supported(o, i, T):
+        return False
+    # a K-range's rows must fit the kernel's 32-bit buffer offsets
+    splits = int(_lib.lib().dtd_wgrad_tn_splits(o, i, T))
+    rows = -(-T // 32 // splits) * 32
+    return rows * max(dy.stride(0), x.stride(0)) * 2 < 0x7FFFFFFF
 
 
 def wgrad_tn(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None, variant: int = 0) -> torch.Tensor:
