@@ -53,9 +53,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="base")
-    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("DTD_BENCH_BATCH", "512")),
-                    help="per-GPU micro-batch (sequences); 512 x 512 tokens use 81 GB of the 288 GB "
-                         "(+1.5 %% tokens/s over 256 on the same box, profiles/r5_s39_batch.jsonl)")
+    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("DTD_BENCH_BATCH", "1024")),
+                    help="per-GPU micro-batch (sequences); 1024 x 512 tokens use 161 GB of the 288 GB "
+                         "(same box: 256 / 512 / 768 / 1024 -> 1.471 / 1.498 / 1.506 / 1.510 M tokens/s, "
+                         "profiles/r5_s39_batch.jsonl)")
     ap.add_argument("--seq-len", type=int, default=512)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--grad-dtype", default=None, choices=[None, "bf16", "fp32"])
