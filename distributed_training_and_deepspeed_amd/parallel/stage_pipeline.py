@@ -9,7 +9,9 @@ module groups), activations travel forward and their gradients backward as point
 messages (RCCL send/recv over xGMI on GPUs; staged through host memory on gloo), and every rank
 issues only its own stage's kernels -- no host thread drives several GPUs, so the step is not
 host-issue-bound, and each rank's step is a fixed kernel + message sequence that can be
-captured as one hipGraph per stage (``capture=True``).
+captured as one hipGraph per stage (``utils/graphs.CapturedStep`` around ``train_step`` + the
+optimizer: ``model_parallel_training.py --graph on`` under torchrun with RCCL; gloo stages
+messages through host memory and is not capturable).
 
 Schedules (``schedule``):
   * ``gpipe``: fill-drain (torch Pipe's): all micro-batch forwards, then all backwards;
