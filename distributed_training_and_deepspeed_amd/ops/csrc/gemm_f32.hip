@@ -5,19 +5,26 @@
 // fp32 FMA chain at 64 FLOP/clk/SIMD, the same rate as the f32 VALU (cdna_hip_programming.md §3
 // "FP32-input MFMA").  At that rate one 32x32x2 MFMA (4096 FLOP) takes 64 cycles and consumes
 // 512 B of operands, so the kernel is MFMA-bound by a wide margin: LDS bandwidth, load latency and
-// the epilogue are secondary, and a plain structure reaches the pipe -- 128x128 tiles, 4 waves of
-// 64x64 (2x2 blocks of 32x32, 64 accumulator registers per lane), 16-deep K-steps double-buffered
-// in LDS, up to 3 workgroups per CU so one workgroup's loads and barrier hide under another's MFMAs.
+// the epilogue are secondary -- 128x128 tiles, 4 waves of 64x64 (2x2 blocks of 32x32, 64
+// accumulator registers per lane), 32-deep K-steps double-buffered in LDS (72 KiB), 2 workgroups
+// per CU so one workgroup's loads and barrier hide under the other's MFMAs.
 //
 //   NT: C[M, N] = A[M, K] . B[N, K]^T (+ bias[n])   Linear forward; input gradient with B = W^T
 //   TN: C[M, N] = A[K, M]^T . B[K, N]              weight gradient dW = dY^T X (K = tokens), with
 //       an optional split over K into fp32 partial slices (summed by ops/csrc/reduce.hip)
 //
-// Fragment k order: a 16-deep K-step is 8 MFMA steps; lane half h takes k = 8h + s in step s, so an
-// NT operand row is read as two float4 (rows padded to 20 floats: the 16 rows of a ds_read_b128
-// lane group land on distinct 4-bank slots).  TN operands are staged as [k][m] rows (pitch 132
-// floats) and read one float per step, 32 consecutive m per half-wave (conflict-free).
+// One LDS layout for both forms: each operand tile is staged as [row][k] (128 rows x 32 k, row
+// pitch 36 floats), so the fragment reads are ds_read_b128 of 4 consecutive k in either form; the
+// TN form transposes while writing LDS (4 scalar writes per global float4).  A 32-deep K-step is 16
+// MFMA steps: lane half h takes k = 16h + s in step s, i.e. 4 float4 per fragment row (the 16 rows
+// of a ds_read_b128 lane group land on distinct 4-bank slots: pitch / 4 is odd).
+// Round 5 (profiles/r5_s49_f32_gemm.jsonl): the 16-deep form with 3 workgroups per CU kept the f32
+// MFMA pipe 78 % (NT) / 61 % (TN) busy against hipBLASLt's 83-91 % at the same 2.4 GHz clock --
+// one barrier per 2048 MFMA cycles and, in TN, 32 scalar LDS reads per K-step; 32-deep steps at 2
+// workgroups per CU halve the barriers and give TN the NT read path.
 // C/D map: register i of lane l is row crow(i, l >> 5), column l & 31 of a 32x32 block.
+#include <cmath>
+
 #include "common.h"
 
 using namespace dtd;
@@ -26,10 +33,9 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BN = 128, BK = 16;
-constexpr int NT_PITCH = BK + 4;          // floats per staged row, NT layout
-constexpr int TN_PITCH = BM + 4;          // floats per staged k-row, TN layout (BM == BN)
-constexpr int STAGE_FLOATS = 2 * BM * NT_PITCH > 2 * BK * TN_PITCH ? 2 * BM * NT_PITCH : 2 * BK * TN_PITCH;
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int PITCH = BK + 4;             // floats per staged row ([row][k], both forms)
+constexpr int OP_FLOATS = BM * PITCH;     // one operand tile (BM == BN)
 
 __device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -53,60 +59,99 @@ __device__ __forceinline__ void tile_xy(int& bm, int& bn, int ntn) {
   bn = t % ntn;
 }
 
-template <bool TN>
-__global__ void __launch_bounds__(256, 3) gemm_f32_kernel(F32GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float sm[2][STAGE_FLOATS];
+// BNT: N-width of the workgroup tile, 128 (waves 2 x 2 of 64 x 64) or 64 (waves 2 x 2 of 64 x 32:
+// twice the tiles, for shapes whose 128-wide grid leaves the last round of 2 workgroups per CU
+// half empty -- N = 768 at 16k tokens is 1.5 rounds).  The TN form uses 128 only.
+template <bool TN, int BNT>
+__global__ void __launch_bounds__(256, 2) gemm_f32_kernel(F32GemmArgs g) {
+  static_assert(BNT == 128 || (BNT == 64 && !TN), "tile width");
+  constexpr int NJ = BNT / 64;            // 32-column B blocks per wave
+  constexpr int NB = BNT / 32;            // B float4 loads per thread per K-step (NT)
+  __shared__ __attribute__((aligned(16))) float sm[2][OP_FLOATS + BNT * PITCH];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
-  const int ntn = g.N / BN;
+  const int ntn = g.N / BNT;
   int bm, bn;
   tile_xy(bm, bn, ntn);
-  const int m0 = bm * BM, n0 = bn * BN;
+  const int m0 = bm * BM, n0 = bn * BNT;
   const int nk_all = g.K / BK;
   const int kb = blockIdx.z * g.ksplit;
   const int nk = min(g.ksplit, nk_all - kb);
   float* cbase = g.c + (size_t)blockIdx.z * g.cstride;
 
-  // global -> registers: 2 float4 of A and 2 of B per thread per K-step (named, not an array: a
-  // runtime-indexed array lands in scratch).
-  // NT: 128 rows x 16 floats per operand = 512 float4: thread t takes rows t/4 and t/4 + 64, chunk t%4
-  // TN: 16 k-rows x 128 floats = 512 float4: thread t takes k-rows t/32 and t/32 + 8, chunk t%32
-  float4 ra0, ra1, rb0, rb1;
-  const int q_row = TN ? tid / 32 : tid / 4, q_ch = TN ? tid % 32 : tid % 4, q_step = TN ? 8 : 64;
+  // global -> registers: 4 float4 of A and 4 of B per thread per K-step (named, not an array: a
+  // runtime-indexed array lands in scratch).  Each operand tile is 1024 float4.
+  // NT ([row][k] in memory): thread t takes rows t/8 + 32j, k-chunk t%8 (8 lanes = one 128-B row run)
+  // TN ([k][row] in memory): thread t takes k-rows t%8 + 8j, row-chunk t/8 (8 lanes = 8 k-rows of
+  //   one 16-B column run; the wave covers 8 k-rows x 128 B)
+  float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
+  const int q_lo = tid & 7, q_hi = tid >> 3;
   auto gload = [&](int kt) {
     const int k0 = (kb + kt) * BK;
     if constexpr (!TN) {
-      const float* pa = g.a + (size_t)(m0 + q_row) * g.lda + k0 + 4 * q_ch;
-      const float* pb = g.b + (size_t)(n0 + q_row) * g.ldb + k0 + 4 * q_ch;
+      const float* pa = g.a + (size_t)(m0 + q_hi) * g.lda + k0 + 4 * q_lo;
+      const float* pb = g.b + (size_t)(n0 + q_hi) * g.ldb + k0 + 4 * q_lo;
+      const size_t sa = (size_t)32 * g.lda, sb = (size_t)32 * g.ldb;
       ra0 = *reinterpret_cast<const float4*>(pa);
-      ra1 = *reinterpret_cast<const float4*>(pa + (size_t)q_step * g.lda);
+      ra1 = *reinterpret_cast<const float4*>(pa + sa);
+      ra2 = *reinterpret_cast<const float4*>(pa + 2 * sa);
+      ra3 = *reinterpret_cast<const float4*>(pa + 3 * sa);
       rb0 = *reinterpret_cast<const float4*>(pb);
-      rb1 = *reinterpret_cast<const float4*>(pb + (size_t)q_step * g.ldb);
+      rb1 = *reinterpret_cast<const float4*>(pb + sb);
+      if constexpr (NB > 2) {
+        rb2 = *reinterpret_cast<const float4*>(pb + 2 * sb);
+        rb3 = *reinterpret_cast<const float4*>(pb + 3 * sb);
+      }
     } else {
-      const float* pa = g.a + (size_t)(k0 + q_row) * g.lda + m0 + 4 * q_ch;
-      const float* pb = g.b + (size_t)(k0 + q_row) * g.ldb + n0 + 4 * q_ch;
+      const float* pa = g.a + (size_t)(k0 + q_lo) * g.lda + m0 + 4 * q_hi;
+      const float* pb = g.b + (size_t)(k0 + q_lo) * g.ldb + n0 + 4 * q_hi;
+      const size_t sa = (size_t)8 * g.lda, sb = (size_t)8 * g.ldb;
       ra0 = *reinterpret_cast<const float4*>(pa);
-      ra1 = *reinterpret_cast<const float4*>(pa + (size_t)q_step * g.lda);
+      ra1 = *reinterpret_cast<const float4*>(pa + sa);
+      ra2 = *reinterpret_cast<const float4*>(pa + 2 * sa);
+      ra3 = *reinterpret_cast<const float4*>(pa + 3 * sa);
       rb0 = *reinterpret_cast<const float4*>(pb);
-      rb1 = *reinterpret_cast<const float4*>(pb + (size_t)q_step * g.ldb);
+      rb1 = *reinterpret_cast<const float4*>(pb + sb);
+      rb2 = *reinterpret_cast<const float4*>(pb + 2 * sb);
+      rb3 = *reinterpret_cast<const float4*>(pb + 3 * sb);
     }
   };
   auto swrite = [&](float* s) {
-    constexpr int P = TN ? TN_PITCH : NT_PITCH;
-    constexpr int BOFF = TN ? BK * TN_PITCH : BM * NT_PITCH;
-    float* d = s + q_row * P + 4 * q_ch;
-    *reinterpret_cast<float4*>(d) = ra0;
-    *reinterpret_cast<float4*>(d + q_step * P) = ra1;
-    *reinterpret_cast<float4*>(d + BOFF) = rb0;
-    *reinterpret_cast<float4*>(d + BOFF + q_step * P) = rb1;
+    if constexpr (!TN) {
+      float* d = s + q_hi * PITCH + 4 * q_lo;
+      *reinterpret_cast<float4*>(d) = ra0;
+      *reinterpret_cast<float4*>(d + 32 * PITCH) = ra1;
+      *reinterpret_cast<float4*>(d + 64 * PITCH) = ra2;
+      *reinterpret_cast<float4*>(d + 96 * PITCH) = ra3;
+      d += OP_FLOATS;
+      *reinterpret_cast<float4*>(d) = rb0;
+      *reinterpret_cast<float4*>(d + 32 * PITCH) = rb1;
+      if constexpr (NB > 2) {
+        *reinterpret_cast<float4*>(d + 64 * PITCH) = rb2;
+        *reinterpret_cast<float4*>(d + 96 * PITCH) = rb3;
+      }
+    } else {
+      // element (k = q_lo + 8j, row = 4 q_hi + c) -> [row][k]; lanes of one write spread over 32
+      // banks (2-way at most)
+      float* d = s + 4 * q_hi * PITCH + q_lo;
+      auto put = [&](float* base, const float4& v, int j) {
+        base[0 * PITCH + 8 * j] = v.x;
+        base[1 * PITCH + 8 * j] = v.y;
+        base[2 * PITCH + 8 * j] = v.z;
+        base[3 * PITCH + 8 * j] = v.w;
+      };
+      put(d, ra0, 0); put(d, ra1, 1); put(d, ra2, 2); put(d, ra3, 3);
+      d += OP_FLOATS;
+      put(d, rb0, 0); put(d, rb1, 1); put(d, rb2, 2); put(d, rb3, 3);
+    }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
 
   if (nk > 0) {
     gload(0);
@@ -116,56 +161,45 @@ __global__ void __launch_bounds__(256, 3) gemm_f32_kernel(F32GemmArgs g) {
   for (int kt = 0; kt < nk; ++kt) {
     const float* s = sm[kt & 1];
     if (kt + 1 < nk) gload(kt + 1);   // lands under this K-step's MFMAs
-    if constexpr (!TN) {
-      // A / B fragments: rows (block * 32 + r), k = 8 hh .. 8 hh + 7 as two float4
-      float4 fa[2][2], fb[2][2];
+    // two halves of 8 MFMA steps; fragments: rows (block * 32 + r), k = 16 hh + 8 half .. + 7
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int half = 0; half < 2; ++half) {
+      float4 fa[2][2], fb[NJ][2];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          fa[i][c] = *reinterpret_cast<const float4*>(s + (wm * 64 + i * 32 + r) * NT_PITCH + 8 * hh + 4 * c);
-          fb[i][c] = *reinterpret_cast<const float4*>(s + BM * NT_PITCH + (wn * 64 + i * 32 + r) * NT_PITCH + 8 * hh + 4 * c);
-        }
+      for (int c = 0; c < 2; ++c) {
+        const int k = 16 * hh + 8 * half + 4 * c;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          fa[i][c] = *reinterpret_cast<const float4*>(s + (wm * 64 + i * 32 + r) * PITCH + k);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          fb[j][c] = *reinterpret_cast<const float4*>(s + OP_FLOATS + (wn * 32 * NJ + j * 32 + r) * PITCH + k);
+      }
 #pragma unroll
       for (int st = 0; st < 8; ++st)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < NJ; ++j)
             // transposed tile (B operand first): lane column = m, register rows = n
             acc[i][j] = mfma_f32(comp(fb[j][st >> 2], st & 3), comp(fa[i][st >> 2], st & 3), acc[i][j]);
-    } else {
-#pragma unroll
-      for (int st = 0; st < 8; ++st) {
-        const int k = 8 * hh + st;
-        float fa[2], fb[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          fa[i] = s[k * TN_PITCH + wm * 64 + i * 32 + r];
-          fb[i] = s[BK * TN_PITCH + k * TN_PITCH + wn * 64 + i * 32 + r];
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma_f32(fb[j], fa[i], acc[i][j]);
-      }
     }
     if (kt + 1 < nk) {
       swrite(sm[(kt + 1) & 1]);
       __syncthreads();
     }
   }
-  // lane holds C[m = m0 + wm*64 + i*32 + r][n = n0 + wn*64 + j*32 + crow(reg, hh)]; registers
+  // lane holds C[m = m0 + wm*64 + i*32 + r][n = n0 + wn*32*NJ + j*32 + crow(reg, hh)]; registers
   // 4g .. 4g+3 are 4 consecutive n of one row: one float4 store each (the epilogue is a rounding
   // error next to the f32-MFMA main loop)
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = m0 + wm * 64 + i * 32 + r;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
-        const int n = n0 + wn * 64 + j * 32 + 8 * gq + 4 * hh;
+        const int n = n0 + wn * 32 * NJ + j * 32 + 8 * gq + 4 * hh;
         float4 v = make_float4(acc[i][j][4 * gq], acc[i][j][4 * gq + 1], acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
         if (!TN && g.bias) {
           const float4 bv = *reinterpret_cast<const float4*>(g.bias + n);
@@ -194,23 +228,42 @@ DTD_EXPORT int dtd_gemm_f32_supported(int M, int N, int K) {
   return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0;
 }
 
-// NT: a [M, K] (lda), b [N, K] (ldb) -> c [M, N] (ldc) (+ bias [N])
+// fraction of the launched workgroup slots (2 per CU) a grid of `wgs` workgroups keeps busy
+double slot_use(double wgs) {
+  const double slots = 2.0 * f32_num_cus();
+  return wgs / (std::ceil(wgs / slots) * slots);
+}
+
+// NT: a [M, K] (lda), b [N, K] (ldb) -> c [M, N] (ldc) (+ bias [N]); 128- or 64-wide tiles, whichever
+// fills the last round better
 DTD_EXPORT int dtd_gemm_f32_nt(const float* a, int lda, const float* b, int ldb, float* c, int ldc, const float* bias,
                                int M, int N, int K, hipStream_t s) {
   if (!dtd_gemm_f32_supported(M, N, K) || lda % 4 || ldb % 4 || ldc % 4 || lda < K || ldb < K || ldc < N)
     return (int)hipErrorInvalidValue;
   F32GemmArgs g{a, b, c, bias, M, N, K, lda, ldb, ldc, K / BK, 0};
-  hipLaunchKernelGGL((gemm_f32_kernel<false>), dim3((M / BM) * (N / BN), 1, 1), dim3(256), 0, s, g);
+  const int t128 = (M / BM) * (N / 128);
+  if (slot_use(2.0 * t128) > slot_use(t128) + 0.02)
+    hipLaunchKernelGGL((gemm_f32_kernel<false, 64>), dim3(2 * t128, 1, 1), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<false, 128>), dim3(t128, 1, 1), dim3(256), 0, s, g);
   DTD_LAUNCH_CHECK();
 }
 
-// split count for a TN product: about two workgroups per CU over all splits
+// split count for a TN product: minimises (rounds of 2 workgroups per CU) x (K-steps per split) plus
+// the split-K reduce's extra HBM traffic (one M x N fp32 slice per split), in units of one
+// workgroup K-step (~3.8 us at 140 TF/s) vs ~4 TB/s for the reduce
 DTD_EXPORT int dtd_gemm_f32_tn_splits(int M, int N, int K) {
   const int tiles = (M / BM) * (N / BN), nk = K / BK;
-  int sp = (2 * f32_num_cus() + tiles - 1) / tiles;
-  if (sp < 1) sp = 1;
-  if (sp > nk) sp = nk;
-  return sp;
+  const double slots = 2.0 * f32_num_cus();
+  const double kstep_us = 3.8, slice_us = (double)M * N * 4 / 4e6;
+  int best = 1;
+  double best_t = 1e300;
+  for (int sp = 1; sp <= nk && sp <= 64; ++sp) {
+    const int ks = (nk + sp - 1) / sp, sp_eff = (nk + ks - 1) / ks;
+    const double t = std::ceil((double)tiles * sp_eff / slots) * ks * kstep_us + (sp_eff > 1 ? (sp_eff + 1) * slice_us : 0.0);
+    if (t < best_t - 1e-9) { best_t = t; best = sp_eff; }
+  }
+  return best;
 }
 
 // TN: a [K, M] (lda), b [K, N] (ldb) -> part [splits][M][N] fp32 partial products over contiguous
@@ -221,6 +274,6 @@ DTD_EXPORT int dtd_gemm_f32_tn(const float* a, int lda, const float* b, int ldb,
     return (int)hipErrorInvalidValue;
   const int nk = K / BK, ks = (nk + splits - 1) / splits;
   F32GemmArgs g{a, b, part, nullptr, M, N, K, lda, ldb, N, ks, (long long)M * N};
-  hipLaunchKernelGGL((gemm_f32_kernel<true>), dim3((M / BM) * (N / BN), 1, splits), dim3(256), 0, s, g);
+  hipLaunchKernelGGL((gemm_f32_kernel<true, 128>), dim3((M / BM) * (N / BN), 1, splits), dim3(256), 0, s, g);
   DTD_LAUNCH_CHECK();
 }

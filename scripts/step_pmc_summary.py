@@ -17,12 +17,12 @@ from collections import defaultdict
 def family(name: str) -> str:
     if "Cijk" in name:
         return "hipBLASLt GEMM"
-    m = re.search(r"(gemm_bt_persistent<\d+|gemm_tn\w*|attn_\w+_kernel\w*|ln_\w+_wave|emb_ln_fwd_wave|adam_kernel|xent_\w+_kernel|"
+    m = re.search(r"(gemm_bt_persistent<\d+|gemm_f32_kernel<\w+>|wgrad_tn_kernel|gemm_tn\w*|attn_\w+_kernel\w*|ln_\w+_wave|emb_ln_fwd_wave|adam_kernel|xent_\w+_kernel|"
                   r"splitk_reduce_kernel|embed_\w+_kernel|colsum_finalize_kernel|act_\w+_kernel|dropout_kernel)", name)
     return m.group(1) if m else "other"
 
 
-def main(path, steps):
+def main(path, steps, by_name=False):
     per = defaultdict(dict)
     for r in csv.DictReader(open(path)):
         key = (r["Dispatch_Id"], r["Kernel_Name"])
@@ -30,7 +30,7 @@ def main(path, steps):
         per[key]["_dur"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     fam = defaultdict(lambda: defaultdict(float))
     for (_, name), c in per.items():
-        f = fam[family(name)]
+        f = fam[name[:110] if by_name else family(name)]
         f["n"] += 1
         f["dur"] += c["_dur"]
         f["cyc"] += c.get("GRBM_GUI_ACTIVE", 0) / 8
@@ -54,4 +54,5 @@ def main(path, steps):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 1.0)
+    # a third argument "name" groups by kernel name instead of family
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 1.0, len(sys.argv) > 3 and sys.argv[3] == "name")

@@ -17,13 +17,16 @@ def rel(a, b):
 
 @pytest.fixture
 def f32_on():
+    prev = (G._F32[0], G._F32_WGRAD[0])
     G.set_f32(True)
     yield
-    G.set_f32(False, wgrad=True)          # back to the default: weight gradients only
+    G.set_f32(*prev)                      # back to the process default (DTD_GEMM_F32)
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 128, 16), (256, 384, 64), (512, 768, 768), (1024, 3072, 768),
-                                   (768, 768, 3072)])
+# the smaller grids launch 64-wide tiles (they fill the last round of 2 workgroups per CU better);
+# 8192 x 1024 is exactly 512 128-wide tiles and takes the 128-wide form
+@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (256, 384, 64), (512, 768, 768), (1024, 3072, 768),
+                                   (768, 768, 3072), (8192, 1024, 256)])
 def test_gemm_f32_nt_matches_fp64(f32_on, M, N, K):
     torch.manual_seed(0)
     a = torch.randn(M, K, device="cuda")
@@ -74,6 +77,7 @@ def test_fp32_model_path_matches_library(f32_on):
     from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
     from distributed_training_and_deepspeed_amd.models import build_model
     out = []
+    prev = (G._F32[0], G._F32_WGRAD[0])
     for on in (False, True):
         G.set_f32(on)                     # off: library everywhere; on: every fp32 product hand-written
         model = build_model("bert-tiny", impl="fused", dtype=torch.float32, device="cuda", seed=5)
@@ -83,6 +87,7 @@ def test_fp32_model_path_matches_library(f32_on):
         torch.cuda.synchronize()
         out.append((loss.item(), {n: p.grad.double().clone() for n, p in model.named_parameters()
                                   if p.grad is not None}))
+    G.set_f32(*prev)
     (l0, g0), (l1, g1) = out
     assert abs(l0 - l1) < 1e-5 * abs(l0)
     assert g0.keys() == g1.keys()
