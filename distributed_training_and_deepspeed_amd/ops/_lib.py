@@ -88,7 +88,10 @@ _SIGS = {
     "dtd_wgrad_tn": (I, [I, P, I, P, I, P, I, I, I, I, P]),
     # gemm_f32.hip
     "dtd_gemm_f32_supported": (I, [I, I, I]),
-    "dtd_gemm_f32_nt": (I, [P, I, P, I, P, I, P, I, I, I, P]),
+    "dtd_gemm_f32_set_kernel": (I, [I]),
+    "dtd_gemm_f32_nt": (I, [P, I, P, I, P, I, P, I, I, I, I, P]),
+    "dtd_gemm_f32_nn": (I, [P, I, P, I, P, I, I, I, I, I, P]),
+    "dtd_transpose_many_f32": (I, [P, P, P, P, I, P]),
     "dtd_gemm_f32_tn_splits": (I, [I, I, I]),
     "dtd_gemm_f32_tn": (I, [P, I, P, I, P, I, I, I, I, P]),
     # gemm_ln.hip

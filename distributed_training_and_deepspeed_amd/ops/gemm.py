@@ -109,15 +109,21 @@ def set_all(on: bool) -> None:
     _ALL[0] = bool(on)
 
 
-# fp32 (reference-precision) products on the hand-written f32-MFMA kernel (ops/csrc/gemm_f32.hip).
-# DTD_GEMM_F32 = "wgrad": the split-K weight gradients only; "1"/"all": every fp32 product; "0"
-# (default): none.  Measured (profiles/r4_s2c_results.jsonl, r4_fp32_b32_kernel_summary.txt): the
-# library's forward / input-gradient GEMMs run at 123-149 TF/s against the hand kernel's 110-123;
-# the hand TN kernel beats a single-call library wgrad (87-98 vs 64 TF/s) but in the step it runs at
-# ~96 TF/s, slower than the library's K-sliced bmm path the step uses -- so all stay opt-in.
-_F32_MODE = os.environ.get("DTD_GEMM_F32", "0")
+# fp32 (reference-precision) products on the hand-written f32-MFMA kernels (ops/csrc/gemm_f32.hip).
+# DTD_GEMM_F32 = "wgrad" (default): the split-K weight gradients; "1"/"all": every fp32 product; "0":
+# none.  Round 5 (profiles/r5_s49_f32_gemm.jsonl, BERT-base fp32 b32 on one MI355X): the register-
+# direct kernels run the weight gradients at 107-135 TF/s vs hipBLASLt's 98-132 at 16k tokens (118-131
+# vs 64 at 32k) and the forward products at 121-146 vs 117-149 -- in the step the weight-gradient
+# mode is at parity or better (190.1-191.4 k vs 189.9-190.7 k tokens/s) while every-product mode is
+# 2 % behind (186.4 k): the kernels co-running on side streams (keep-mask generator, staged Adam)
+# slow down beside a 512-register wave, so forward / input gradients stay on the library by default.
+_F32_MODE = os.environ.get("DTD_GEMM_F32", "wgrad")
 _F32 = [_F32_MODE in ("1", "all")]
 _F32_WGRAD = [_F32_MODE in ("1", "all", "wgrad")]
+# fp32 input gradients: NT on the step's batched W^T copies (default; both operands in the blocked
+# [row][k] layout, 0.86-0.89 MFMA-busy) or NN straight from W (DTD_GEMM_F32_DGRAD=nn; the
+# [k][n] operand runs 0.77-0.84, profiles/r5_s49_f32_gemm.jsonl)
+_F32_DGRAD_NN = os.environ.get("DTD_GEMM_F32_DGRAD", "nt") == "nn"
 
 
 def set_f32(on: bool, wgrad: bool | None = None) -> None:
@@ -125,6 +131,13 @@ def set_f32(on: bool, wgrad: bool | None = None) -> None:
     separately (default: follow ``on``)."""
     _F32[0] = bool(on)
     _F32_WGRAD[0] = bool(on) if wgrad is None else bool(wgrad)
+
+
+def set_f32_kernel(form: str = "auto") -> None:
+    """Which hand-written fp32 form runs: "reg" (register-direct, one wave per workgroup), "lds"
+    (LDS-staged, 2 workgroups per CU) or "auto" (the register form where its grid fills a round;
+    ``DTD_GEMM_F32_KERNEL`` sets the process default)."""
+    _lib.call("dtd_gemm_f32_set_kernel", {"auto": 0, "lds": 1, "reg": 2}[form])
 
 
 def _ok32(t: torch.Tensor) -> bool:
@@ -138,13 +151,25 @@ def f32_supported(M: int, N: int, K: int, *tensors, wgrad: bool = False) -> bool
     return bool(_lib.lib().dtd_gemm_f32_supported(M, N, K))
 
 
-def gemm_f32_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
-    """a . b^T (+ bias), fp32, exact f32 MFMA products."""
+def gemm_f32_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """a . b^T (+ bias), fp32, exact f32 MFMA products; with ``out``: out += a . b^T (+ bias)."""
     M, K = a.shape
     N = b.shape[0]
-    c = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    c = torch.empty((M, N), dtype=torch.float32, device=a.device) if out is None else out
     _lib.call("dtd_gemm_f32_nt", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
-              _lib.ptr(bias), M, N, K, _lib.stream())
+              _lib.ptr(bias), M, N, K, int(out is not None), _lib.stream())
+    return c
+
+
+def gemm_f32_nn(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """a . b for b [K, N] (the input gradient dY W straight from a Linear weight, no transposed
+    copy), fp32; with ``out``: out += a . b."""
+    M, K = a.shape
+    N = b.shape[1]
+    c = torch.empty((M, N), dtype=torch.float32, device=a.device) if out is None else out
+    _lib.call("dtd_gemm_f32_nn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+              M, N, K, int(out is not None), _lib.stream())
     return c
 
 
@@ -375,26 +400,44 @@ def _batchable(w: torch.Tensor, dev) -> bool:
             and w.numel() > 0 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and w.data_ptr() % 16 == 0)
 
 
+def _batchable32(w: torch.Tensor, dev) -> bool:
+    return (_F32[0] and w.is_cuda and w.device == dev and w.dtype == torch.float32 and w.dim() == 2
+            and w.is_contiguous() and w.numel() > 0 and w.shape[0] % 4 == 0 and w.shape[1] % 4 == 0
+            and w.data_ptr() % 16 == 0)
+
+
 def prepare_transposes(weights) -> None:
     """Transpose every eligible weight of ``weights`` (resident, on the current device) in batched
-    launches of up to 64; transposed() then returns the cached copies."""
+    launches of up to 64 -- bf16 weights, and fp32 ones when the hand-written fp32 GEMMs are on;
+    transposed() / the fp32 input-gradient path then take the cached copies."""
     if not (_WT_BATCH[0] and _lib.has("dtd_transpose_many")):
         return
     if any(w.numel() == 0 for w in weights):
         return   # partitioned parameters (ZeRO-3 releases them between uses): per-call transposes
     dev = torch.device("cuda", torch.cuda.current_device())
-    todo = [w for w in weights if _batchable(w, dev) and id(w) not in _WT_CACHE]
-    for k in range(0, len(todo), 64):
-        chunk = todo[k:k + 64]
-        outs = [torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device) for w in chunk]
-        n = len(chunk)
-        ins_a = (ctypes.c_void_p * n)(*[w.data_ptr() for w in chunk])
-        outs_a = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
-        rows_a = (ctypes.c_int * n)(*[w.shape[0] for w in chunk])
-        cols_a = (ctypes.c_int * n)(*[w.shape[1] for w in chunk])
-        _lib.call("dtd_transpose_many", ins_a, outs_a, rows_a, cols_a, n, _lib.stream())
-        for w, o in zip(chunk, outs):
-            _WT_CACHE[id(w)] = (w, w.data_ptr(), o)
+    for fn, ok in (("dtd_transpose_many", _batchable), ("dtd_transpose_many_f32", _batchable32)):
+        if not _lib.has(fn):
+            continue
+        todo = [w for w in weights if ok(w, dev) and id(w) not in _WT_CACHE]
+        for k in range(0, len(todo), 64):
+            chunk = todo[k:k + 64]
+            outs = [torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device) for w in chunk]
+            n = len(chunk)
+            ins_a = (ctypes.c_void_p * n)(*[w.data_ptr() for w in chunk])
+            outs_a = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+            rows_a = (ctypes.c_int * n)(*[w.shape[0] for w in chunk])
+            cols_a = (ctypes.c_int * n)(*[w.shape[1] for w in chunk])
+            _lib.call(fn, ins_a, outs_a, rows_a, cols_a, n, _lib.stream())
+            for w, o in zip(chunk, outs):
+                _WT_CACHE[id(w)] = (w, w.data_ptr(), o)
+
+
+def _t32(w: torch.Tensor) -> torch.Tensor | None:
+    """W^T of an fp32 weight from this backward's batched transposes (handed out once), or None."""
+    e = _WT_CACHE.pop(id(w), None)
+    if e is not None and e[0] is w and e[1] == w.data_ptr():
+        return e[2]
+    return None
 
 
 def transposed(w: torch.Tensor) -> torch.Tensor:
@@ -415,19 +458,12 @@ def _ok1d32(t: torch.Tensor) -> bool:
     return t.is_cuda and t.dtype == torch.float32 and t.dim() == 1 and t.is_contiguous() and t.data_ptr() % 16 == 0
 
 
-def _t32(w: torch.Tensor) -> torch.Tensor:
-    """W^T of an fp32 weight (contiguous), cached for this backward like the bf16 copies."""
-    e = _WT_CACHE.pop(id(w), None)
-    if e is not None and e[0] is w and e[1] == w.data_ptr():
-        return e[2]
-    return w.t().contiguous()
-
-
 def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dy @ w for a Linear weight w [out, in], through the NT form when it applies (the
     hand-written kernel in the all-native mode; the fp32 kernel for fp32 operands)."""
     if dy.dtype == torch.float32 and dy.dim() == 2 and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w):
-        return gemm_f32_nt(dy, _t32(w))
+        wt = _t32(w)
+        return gemm_f32_nn(dy, w) if wt is None or _F32_DGRAD_NN else gemm_f32_nt(dy, wt)
     wt = transposed_for_dgrad(w)
     if wt is None:
         return dy @ w
@@ -439,7 +475,8 @@ def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 def dgrad_add_(c: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """c += dy @ w in place (residual-branch input gradient), NT form when it applies."""
     if dy.dtype == torch.float32 and dy.dim() == 2 and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w, c):
-        return c.add_(gemm_f32_nt(dy, _t32(w)))
+        wt = _t32(w)
+        return gemm_f32_nn(dy, w, out=c) if wt is None or _F32_DGRAD_NN else gemm_f32_nt(dy, wt, out=c)
     wt = transposed_for_dgrad(w)
     if wt is None:
         return c.addmm_(dy, w)

@@ -59,6 +59,16 @@ def main():
         t = statistics.median([timed(lambda k=k: G.gemm_f32_tn(dy[k], xin[k]).sum(0)) for _ in range(3)])
         out["hand_wgrad_" + k] = {"us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
         print(json.dumps({k: [out["wgrad_" + k], out["hand_wgrad_" + k]]}), flush=True)
+    # input gradients dY W [out, in]: library matmul vs the hand NN form (no transposed weight copy)
+    for k in ("qkv", "o", "fc1", "fc2"):
+        wk = w[k]
+        d = dy[k] if k in ("qkv", "fc1") else (x if k == "o" else x)
+        fl = 2 * T * wk.shape[0] * wk.shape[1]
+        t = statistics.median([timed(lambda d=d, wk=wk: d @ wk) for _ in range(3)])
+        out["dgrad_" + k] = {"us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
+        t = statistics.median([timed(lambda d=d, wk=wk: G.gemm_f32_nn(d, wk)) for _ in range(3)])
+        out["hand_dgrad_" + k] = {"us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
+        print(json.dumps({"dgrad_" + k: [out["dgrad_" + k], out["hand_dgrad_" + k]]}), flush=True)
     # the same with TF32-like reduced precision explicitly off (torch's default for fp32 matmul)
     print(json.dumps({"T": T, "allow_tf32": torch.backends.cuda.matmul.allow_tf32, "results": out}), flush=True)
 

@@ -15,16 +15,20 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
 
 
-@pytest.fixture
-def f32_on():
+@pytest.fixture(params=["reg", "lds"])
+def f32_on(request):
+    """Every case runs on both hand-written forms (the register-direct and the LDS-staged kernel)."""
     prev = (G._F32[0], G._F32_WGRAD[0])
     G.set_f32(True)
+    G.set_f32_kernel(request.param)
     yield
+    G.set_f32_kernel("auto")
     G.set_f32(*prev)                      # back to the process default (DTD_GEMM_F32)
 
 
-# the smaller grids launch 64-wide tiles (they fill the last round of 2 workgroups per CU better);
-# 8192 x 1024 is exactly 512 128-wide tiles and takes the 128-wide form
+# LDS form: the smaller grids launch 64-wide tiles (they fill the last round of 2 workgroups per CU
+# better), 8192 x 1024 is exactly 512 128-wide tiles and takes the 128-wide form; register form:
+# 768-wide products take 128 x 96 wave tiles, the others 128 x 128
 @pytest.mark.parametrize("M,N,K", [(128, 128, 32), (256, 384, 64), (512, 768, 768), (1024, 3072, 768),
                                    (768, 768, 3072), (8192, 1024, 256)])
 def test_gemm_f32_nt_matches_fp64(f32_on, M, N, K):
@@ -49,6 +53,44 @@ def test_gemm_f32_nt_strided_and_asymmetric(f32_on):
     b = big[:, :n]                                   # ldb = 2n
     c = G.gemm_f32_nt(eye, b)                        # I . b^T = b^T
     assert torch.equal(c, b.t().contiguous())
+
+
+# NN form (the input gradient dY W straight from the weight): 1024 x 3072 takes 128 x 96 wave tiles
+@pytest.mark.parametrize("M,N,K", [(512, 768, 2304), (1024, 3072, 768), (256, 128, 128)])
+def test_gemm_f32_nn_matches_fp64(f32_on, M, N, K):
+    torch.manual_seed(2)
+    a = torch.randn(M, K, device="cuda")
+    b = torch.randn(K, N, device="cuda")
+    ref = a.double() @ b.double()
+    assert rel(G.gemm_f32_nn(a, b), ref) < 2e-6
+    base = torch.randn(M, N, device="cuda")
+    out = base.clone()
+    G.gemm_f32_nn(a, b, out=out)
+    assert rel(out, ref + base.double()) < 2e-6
+
+
+def test_transpose_many_f32_exact(f32_on):
+    """The batched fp32 W^T copies the input-gradient NT form reads (ops/gemm.py::prepare_transposes):
+    exact, over several entries with partial 64 x 64 tiles."""
+    torch.manual_seed(5)
+    ws = [torch.randn(r, c, device="cuda") for r, c in ((2304, 768), (768, 3072), (100, 36), (4, 260))]
+    G.clear_transposes()
+    G.prepare_transposes(ws)
+    for w in ws:
+        wt = G._t32(w)
+        assert wt is not None and torch.equal(wt, w.t()), w.shape
+    G.clear_transposes()
+
+
+def test_gemm_f32_nt_accumulate(f32_on):
+    torch.manual_seed(4)
+    a = torch.randn(1024, 768, device="cuda")
+    b = torch.randn(768, 768, device="cuda")
+    bias = torch.randn(768, device="cuda")
+    base = torch.randn(1024, 768, device="cuda")
+    out = base.clone()
+    G.gemm_f32_nt(a, b, bias, out=out)
+    assert rel(out, a.double() @ b.double().t() + bias.double() + base.double()) < 2e-6
 
 
 @pytest.mark.parametrize("T,o,i,splits", [(512, 256, 128, 1), (4096, 768, 768, None), (8192, 768, 3072, None),
