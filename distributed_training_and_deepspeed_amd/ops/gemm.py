@@ -110,16 +110,19 @@ def set_all(on: bool) -> None:
 
 
 # fp32 (reference-precision) products on the hand-written f32-MFMA kernels (ops/csrc/gemm_f32.hip).
-# DTD_GEMM_F32 = "wgrad" (default): the split-K weight gradients; "1"/"all": every fp32 product; "0":
-# none.  Round 5 (profiles/r5_s49_f32_gemm.jsonl, BERT-base fp32 b32 on one MI355X): the register-
+# DTD_GEMM_F32 = "wgrad" (default): the split-K weight gradients; "fwd": the forward products too;
+# "1"/"all": every fp32 product; "0": none.  Round 5 (profiles/r5_s49_f32_gemm.jsonl, BERT-base fp32 b32 on one MI355X): the register-
 # direct kernels run the weight gradients at 107-135 TF/s vs hipBLASLt's 98-132 at 16k tokens (118-131
 # vs 64 at 32k) and the forward products at 121-146 vs 117-149 -- in the step the weight-gradient
 # mode is at parity or better (190.1-191.4 k vs 189.9-190.7 k tokens/s) while every-product mode is
 # 2 % behind (186.4 k): the kernels co-running on side streams (keep-mask generator, staged Adam)
-# slow down beside a 512-register wave, so forward / input gradients stay on the library by default.
+# slow down beside a 512-register wave, so forward / input gradients stay on the library by default
+# ("fwd" mode: 187.7-187.9 k vs 189.5 k -- the forward's side-stream keep-mask generation is the
+# kernel that waits).
 _F32_MODE = os.environ.get("DTD_GEMM_F32", "wgrad")
-_F32 = [_F32_MODE in ("1", "all")]
-_F32_WGRAD = [_F32_MODE in ("1", "all", "wgrad")]
+_F32 = [_F32_MODE in ("1", "all", "fwd")]
+_F32_WGRAD = [_F32_MODE in ("1", "all", "wgrad", "fwd")]
+_F32_DG = [_F32_MODE in ("1", "all")]        # "fwd": forward + weight gradients, input gradients on the library
 # fp32 input gradients: NT on the step's batched W^T copies (default; both operands in the blocked
 # [row][k] layout, 0.86-0.89 MFMA-busy) or NN straight from W (DTD_GEMM_F32_DGRAD=nn; the
 # [k][n] operand runs 0.77-0.84, profiles/r5_s49_f32_gemm.jsonl)
@@ -129,7 +132,7 @@ _F32_DGRAD_NN = os.environ.get("DTD_GEMM_F32_DGRAD", "nt") == "nn"
 def set_f32(on: bool, wgrad: bool | None = None) -> None:
     """All fp32 products on the hand kernel (on) or none; ``wgrad`` sets the weight gradients
     separately (default: follow ``on``)."""
-    _F32[0] = bool(on)
+    _F32[0] = _F32_DG[0] = bool(on)
     _F32_WGRAD[0] = bool(on) if wgrad is None else bool(wgrad)
 
 
@@ -401,7 +404,7 @@ def _batchable(w: torch.Tensor, dev) -> bool:
 
 
 def _batchable32(w: torch.Tensor, dev) -> bool:
-    return (_F32[0] and w.is_cuda and w.device == dev and w.dtype == torch.float32 and w.dim() == 2
+    return (_F32_DG[0] and w.is_cuda and w.device == dev and w.dtype == torch.float32 and w.dim() == 2
             and w.is_contiguous() and w.numel() > 0 and w.shape[0] % 4 == 0 and w.shape[1] % 4 == 0
             and w.data_ptr() % 16 == 0)
 
@@ -461,7 +464,8 @@ def _ok1d32(t: torch.Tensor) -> bool:
 def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dy @ w for a Linear weight w [out, in], through the NT form when it applies (the
     hand-written kernel in the all-native mode; the fp32 kernel for fp32 operands)."""
-    if dy.dtype == torch.float32 and dy.dim() == 2 and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w):
+    if (dy.dtype == torch.float32 and dy.dim() == 2 and _F32_DG[0]
+            and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w)):
         wt = _t32(w)
         return gemm_f32_nn(dy, w) if wt is None or _F32_DGRAD_NN else gemm_f32_nt(dy, wt)
     wt = transposed_for_dgrad(w)
@@ -474,7 +478,8 @@ def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 def dgrad_add_(c: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """c += dy @ w in place (residual-branch input gradient), NT form when it applies."""
-    if dy.dtype == torch.float32 and dy.dim() == 2 and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w, c):
+    if (dy.dtype == torch.float32 and dy.dim() == 2 and _F32_DG[0]
+            and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w, c)):
         wt = _t32(w)
         return gemm_f32_nn(dy, w, out=c) if wt is None or _F32_DGRAD_NN else gemm_f32_nt(dy, wt, out=c)
     wt = transposed_for_dgrad(w)

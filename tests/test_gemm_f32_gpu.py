@@ -18,12 +18,12 @@ def rel(a, b):
 @pytest.fixture(params=["reg", "lds"])
 def f32_on(request):
     """Every case runs on both hand-written forms (the register-direct and the LDS-staged kernel)."""
-    prev = (G._F32[0], G._F32_WGRAD[0])
+    prev = (G._F32[0], G._F32_WGRAD[0], G._F32_DG[0])
     G.set_f32(True)
     G.set_f32_kernel(request.param)
     yield
     G.set_f32_kernel("auto")
-    G.set_f32(*prev)                      # back to the process default (DTD_GEMM_F32)
+    G._F32[0], G._F32_WGRAD[0], G._F32_DG[0] = prev   # back to the process default (DTD_GEMM_F32)
 
 
 # LDS form: the smaller grids launch 64-wide tiles (they fill the last round of 2 workgroups per CU
@@ -119,7 +119,7 @@ def test_fp32_model_path_matches_library(f32_on):
     from distributed_training_and_deepspeed_amd.data import SyntheticLMDataset
     from distributed_training_and_deepspeed_amd.models import build_model
     out = []
-    prev = (G._F32[0], G._F32_WGRAD[0])
+    prev = (G._F32[0], G._F32_WGRAD[0], G._F32_DG[0])
     for on in (False, True):
         G.set_f32(on)                     # off: library everywhere; on: every fp32 product hand-written
         model = build_model("bert-tiny", impl="fused", dtype=torch.float32, device="cuda", seed=5)
@@ -129,7 +129,7 @@ def test_fp32_model_path_matches_library(f32_on):
         torch.cuda.synchronize()
         out.append((loss.item(), {n: p.grad.double().clone() for n, p in model.named_parameters()
                                   if p.grad is not None}))
-    G.set_f32(*prev)
+    G._F32[0], G._F32_WGRAD[0], G._F32_DG[0] = prev
     (l0, g0), (l1, g1) = out
     assert abs(l0 - l1) < 1e-5 * abs(l0)
     assert g0.keys() == g1.keys()
