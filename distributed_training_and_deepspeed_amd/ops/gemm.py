@@ -115,10 +115,9 @@ def set_all(on: bool) -> None:
 # direct kernels run the weight gradients at 107-135 TF/s vs hipBLASLt's 98-132 at 16k tokens (118-131
 # vs 64 at 32k) and the forward products at 121-146 vs 117-149 -- in the step the weight-gradient
 # mode is at parity or better (190.1-191.4 k vs 189.9-190.7 k tokens/s) while every-product mode is
-# 2 % behind (186.4 k): the kernels co-running on side streams (keep-mask generator, staged Adam)
-# slow down beside a 512-register wave, so forward / input gradients stay on the library by default
-# ("fwd" mode: 187.7-187.9 k vs 189.5 k -- the forward's side-stream keep-mask generation is the
-# kernel that waits).
+# 2 % behind (186.4 k; "fwd" mode 187.7-187.9 k vs 189.5 k): in the step the hand NT products take
+# 41.6 ms against the library's 40.0 although they win in isolation, so forward / input gradients
+# stay on the library by default.
 _F32_MODE = os.environ.get("DTD_GEMM_F32", "wgrad")
 _F32 = [_F32_MODE in ("1", "all", "fwd")]
 _F32_WGRAD = [_F32_MODE in ("1", "all", "wgrad", "fwd")]
