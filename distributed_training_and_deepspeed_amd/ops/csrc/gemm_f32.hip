@@ -258,17 +258,20 @@ struct RegOp<false, NBLK> {             // [row][k]
 };
 template <int NBLK>
 struct RegOp<true, NBLK> {              // [k][row], blocks interleaved
-  float v[8][NBLK];
+  // one 4-float vector per step (3-block form: .xyz): the dwordx3 lands in an aligned register
+  // quad that IS the operand storage -- with 3-float slots hipcc loaded into a temporary and
+  // copied, waiting on the loads it had just issued (the prefetch collapsed)
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  f32x4v v[8];
   __device__ __forceinline__ void load(const float* p, int ld, int row0, int k0, int r, int hh) {
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       const float* q = p + (size_t)(k0 + 8 * hh + st) * ld + row0 + NBLK * r;
       if constexpr (NBLK == 4) {
-        const float4 x = *reinterpret_cast<const float4*>(q);
-        v[st][0] = x.x; v[st][1] = x.y; v[st][2] = x.z; v[st][3] = x.w;
+        v[st] = *reinterpret_cast<const f32x4v*>(q);
       } else {
-#pragma unroll
-        for (int b = 0; b < NBLK; ++b) v[st][b] = q[b];
+        static_assert(NBLK == 3, "block count");
+        v[st].x = q[0]; v[st].y = q[1]; v[st].z = q[2];
       }
     }
   }

@@ -123,9 +123,9 @@ _F32 = [_F32_MODE in ("1", "all", "fwd")]
 _F32_WGRAD = [_F32_MODE in ("1", "all", "wgrad", "fwd")]
 _F32_DG = [_F32_MODE in ("1", "all")]        # "fwd": forward + weight gradients, input gradients on the library
 # fp32 input gradients: NT on the step's batched W^T copies (default; both operands in the blocked
-# [row][k] layout, 0.86-0.89 MFMA-busy) or NN straight from W (DTD_GEMM_F32_DGRAD=nn; the
-# [k][n] operand runs 0.77-0.84, profiles/r5_s49_f32_gemm.jsonl -- with 128 x 96 tiles hipcc also
-# waits on most of the next buffer's dwordx3 loads inside the loop, tests/test_gemm_f32_host_cpu.py)
+# [row][k] layout, 0.86-0.89 MFMA-busy) or NN straight from W (DTD_GEMM_F32_DGRAD=nn: the [k][n]
+# operand costs it 1-2 % of the step even with its loads landing in place, 183.2 k vs 186.5 k,
+# profiles/r5_s49_f32_gemm.jsonl s66)
 _F32_DGRAD_NN = os.environ.get("DTD_GEMM_F32_DGRAD", "nt") == "nn"
 
 

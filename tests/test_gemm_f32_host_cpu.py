@@ -64,17 +64,17 @@ def test_register_kernels_keep_the_prefetch_in_flight(tmp_path):
     out = tmp_path / "gemm_f32.s"
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", os.path.dirname(SRC),
                     "--cuda-device-only", "-S", "-o", str(out), SRC], check=True, capture_output=True)
-    # the NT and TN forms (both operands in the same layout: ILb0ELb0 / ILb1ELb1) -- the ones the
-    # step runs.  The opt-in NN form with 128 x 96 tiles (dwordx3 [k][n] operand) does wait down
-    # to vmcnt(2) after issuing its next buffer, part of why it runs at 0.77 MFMA-busy.
-    bodies = {n: b for n, b in _function_bodies(out.read_text(), "gemm_f32_reg_kernel").items()
-              if "ILb0ELb0E" in n or "ILb1ELb1E" in n}
-    assert len(bodies) >= 3, sorted(bodies)          # NT x 2 tile widths, TN
+    # every form: NT x 2 tile widths, NN x 2, TN.  (The NN form with 128 x 96 tiles once waited down
+    # to vmcnt(2) right after issuing its next buffer: its dwordx3 [k][n] loads landed in a
+    # temporary and were copied into 3-float slots; 4-float vector slots fixed it.)
+    bodies = _function_bodies(out.read_text(), "gemm_f32_reg_kernel")
+    assert len(bodies) >= 5, sorted(bodies)
     for name, lines in bodies.items():
         start = next(k for k, l in enumerate(lines) if "Inner Loop Header" in l)
         end = next(k for k in range(start + 1, len(lines)) if re.search(r"s_cbranch_\w+ \.LBB", lines[k]))
         loop = lines[start:end + 1]
         assert not any("scratch_" in l for l in loop), name
+        assert not any(re.match(r"\s+v_mov_b32", l) for l in loop), name   # no operand copies
         waits = [int(m.group(1)) for l in loop for m in [re.search(r"s_waitcnt vmcnt\((\d+)\)", l)] if m]
         assert waits and min(waits) >= 14, (name, waits)
         assert sum("v_mfma" in l for l in loop) >= 128, name   # both K-steps of the pair
