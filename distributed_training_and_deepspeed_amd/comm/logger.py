@@ -281,6 +281,18 @@ def recv(tensor, src, group=None):
                             tensor, _nbytes(tensor), group, False)
 
 
+def isend(tensor, dst, group=None):
+    """Non-blocking point-to-point send (logged as "send"); returns the work handle."""
+    return comms_logger.run("send", lambda a: dist.isend(tensor, dst=dst, group=group) if a else dist.send(tensor, dst=dst, group=group),
+                            tensor, _nbytes(tensor), group, True)
+
+
+def irecv(tensor, src, group=None):
+    """Non-blocking point-to-point receive into ``tensor`` (logged as "recv"); returns the work handle."""
+    return comms_logger.run("recv", lambda a: dist.irecv(tensor, src=src, group=group) if a else dist.recv(tensor, src=src, group=group),
+                            tensor, _nbytes(tensor), group, True)
+
+
 def barrier(group=None, name: str = "barrier"):
     if not dist.is_initialized():
         return

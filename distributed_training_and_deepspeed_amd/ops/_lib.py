@@ -75,6 +75,9 @@ _SIGS = {
     "dtd_softmax_bwd": (I, [I, P, P, P, I, I, P]),
     # gemm.hip
     "dtd_gemm_bt_supported": (I, [I, I, I]),
+    # gemm_w4.hip
+    "dtd_gemm_w4_supported": (I, [I, I, I]),
+    "dtd_gemm_w4": (I, [I, P, I, P, I, P, I, P, I, I, I, P]),
     "dtd_gemm_bt_part_rows": (I, [I]),
     "dtd_gemm_bt": (I, [I, P, I, P, I, P, I, P, P, I, P, P, I, I, I, P, P]),
     "dtd_spin_occupy": (I, [I, ctypes.c_double, P]),

@@ -167,21 +167,13 @@ def mask_words(B: int, H: int, S: int) -> int:
     return B * H * W * 32 * W
 
 
-def mask_pad_words(S: int) -> int:
-    """Slack after the second layout.  The attention kernels load keep words with unbounded scalar
-    loads: a wave whose 32 queries (keys) lie past the last word row of a tile of up to 256
-    positions still computes its row address (up to 7 rows past W), and the key blocks of the last
-    64-key tile reach up to 63 words past 32 W.  Those words are read and discarded (the scores they
-    select are masked); past the last (batch, head) plane they must still be mapped memory --
-    without the slack S = 64 read 2 rows past the end of the buffer and faulted."""
-    W = (S + 31) // 32
-    return 8 * 32 * W + 256
-
-
 def alloc_masks(B: int, H: int, S: int, device) -> torch.Tensor:
-    """[2, mask_words] int32 keep-bit buffer (both layouts back to back) with the kernels' read slack."""
+    """[2, mask_words] int32 keep-bit buffer (both layouts back to back), exactly sized: every keep
+    word the attention kernels read lies inside it (their scalar-load addresses are clamped into
+    the (batch, head) plane and the row, ops/csrc/attention.hip keep_off; the vector prefetches go
+    through bounded buffer resources)."""
     n = mask_words(B, H, S)
-    return torch.empty(2 * n + mask_pad_words(S), dtype=torch.int32, device=device)[:2 * n].view(2, n)
+    return torch.empty((2, n), dtype=torch.int32, device=device)
 
 
 def _lm_pos(n: int) -> torch.Tensor:

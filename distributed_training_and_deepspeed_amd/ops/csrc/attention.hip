@@ -164,6 +164,10 @@ __device__ __forceinline__ float sel_keep(float v, uint64_t m) {
   return r;
 }
 typedef __attribute__((address_space(4))) const uint64_t cu64;
+// Word offset of a 32-position block's keep words inside its [Sp] row, clamped so the 32 words a
+// scalar load group reads never leave the row (blocks past S -- whose scores are masked, so the
+// words are discarded -- re-read the row's last block instead of running past the buffer).
+__device__ __forceinline__ int keep_off(int off, int Sp) { return min(off, Sp - 32); }
 
 struct FwdArgs {
   const bf16* q; const bf16* k; const bf16* v; bf16* o; float* lse; const float* slopes;
@@ -393,7 +397,9 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
   // of a 32-key block are 16 aligned 64-bit words (lm_pos) -- scalar loads, one v_cndmask per
   // score.  A one-dword-per-lane vector load of the same 64 words a tile ahead pulls them into L2.
   const int Sp = 32 * a.W;
-  const uint32_t* mrow = drop ? a.maskB + ((size_t)bh * a.W + (q0 >> 5)) * Sp : nullptr;
+  // keep-word addresses stay inside the real mask buffer: the row is clamped to the plane (a wave
+  // whose queries lie past S still forms it) and each block's offset to the row (keep_off)
+  const uint32_t* mrow = drop ? a.maskB + ((size_t)bh * a.W + min(q0 >> 5, a.W - 1)) * Sp : nullptr;
   const __amdgpu_buffer_rsrc_t mrs = bounded_rsrc(drop ? (const void*)mrow : (const void*)a.lse, drop ? (uint32_t)Sp * 4u : 0u);
 
   bf16x8 qf[NC];
@@ -447,7 +453,7 @@ __global__ void __launch_bounds__(256, OCC) attn_fwd_kernel(FwdArgs a) {
     // round trip hides under the QK^T / softmax work); the next block's after this one's selects
     uint64_t mk[16];
     auto load_masks = [&](int kb) {
-      const cu64* mp = (const cu64*)(uintptr_t)(mrow + k0 + kb * 32);
+      const cu64* mp = (const cu64*)(uintptr_t)(mrow + keep_off(k0 + kb * 32, Sp));
 #pragma unroll
       for (int i = 0; i < 16; ++i) mk[i] = mp[i];
     };
@@ -842,7 +848,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   // keep masks: this wave's 32 keys are one key word of the query-major layout A, so a 32-query
   // block's masks are 16 aligned 64-bit words (lm_pos) -- scalar loads, one v_cndmask per use
   const int Sp = 32 * a.W;
-  const uint32_t* mrow = drop ? a.maskA + ((size_t)bh * a.W + ((kblk >> 5) + w)) * Sp : nullptr;
+  const uint32_t* mrow = drop ? a.maskA + ((size_t)bh * a.W + min((kblk >> 5) + w, a.W - 1)) * Sp : nullptr;
   const __amdgpu_buffer_rsrc_t mrs = bounded_rsrc(drop ? (const void*)mrow : (const void*)a.lse, drop ? (uint32_t)Sp * 4u : 0u);
   const RowSrc qsrc = row_src<D>(a.q + (size_t)b * S * a.ld + h * D, a.ld, S);
   const RowSrc osrc = row_src<D>(a.dout + (size_t)b * S * a.ldo + h * D, a.ldo, S);
@@ -925,7 +931,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       // this query block's keep masks (after the S / dP MFMAs consumed their LDS operands)
       uint64_t mk[16];
       if constexpr (DROP) {
-        const cu64* mp = (const cu64*)(uintptr_t)(mrow + qrow0);
+        const cu64* mp = (const cu64*)(uintptr_t)(mrow + keep_off(qrow0, Sp));
 #pragma unroll
         for (int i = 0; i < 16; ++i) mk[i] = mp[i];
       }
@@ -1056,7 +1062,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
   const RowSrc vsrc = row_src<D>(a.v + (size_t)b * S * a.ld + h * D, a.ld, S);
   // keep masks as in attn_fwd_kernel: 64-bit lane masks of the key-major layout, scalar loads
   const int Sp = 32 * a.W;
-  const uint32_t* mrow = drop ? a.maskB + ((size_t)bh * a.W + (q0 >> 5)) * Sp : nullptr;
+  const uint32_t* mrow = drop ? a.maskB + ((size_t)bh * a.W + min(q0 >> 5, a.W - 1)) * Sp : nullptr;
   const __amdgpu_buffer_rsrc_t mrs = bounded_rsrc(drop ? (const void*)mrow : (const void*)a.lse, drop ? (uint32_t)Sp * 4u : 0u);
 
   bf16x8 qf[NC], of[NC];
@@ -1139,7 +1145,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dq_kernel(BwdArgs a) {
       // this block's keep masks (after the S / dP MFMAs consumed their LDS operands)
       uint64_t mk[16];
       if (drop) {
-        const cu64* mp = (const cu64*)(uintptr_t)(mrow + k0 + kb * 32);
+        const cu64* mp = (const cu64*)(uintptr_t)(mrow + keep_off(k0 + kb * 32, Sp));
 #pragma unroll
         for (int i = 0; i < 16; ++i) mk[i] = mp[i];
       }
@@ -1382,7 +1388,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_fused_kernel(BwdArgs a) {
         mfma_vgpr_wait(sacc, pacc);
         uint64_t mk[16];
         if constexpr (DROP) {
-          const cu64* mp = (const cu64*)(uintptr_t)(a.maskA + ((size_t)bh * a.W + (w * NKB + kb)) * Sp + q0);
+          const cu64* mp = (const cu64*)(uintptr_t)(a.maskA + ((size_t)bh * a.W + min(w * NKB + kb, a.W - 1)) * Sp +
+                                                    keep_off(q0, Sp));
 #pragma unroll
           for (int i = 0; i < 16; ++i) mk[i] = mp[i];
         }
@@ -1644,7 +1651,8 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_fused8_kernel(BwdArgs a) {
       }
       uint64_t mk[16];
       if constexpr (DROP) {
-        const cu64* mp = (const cu64*)(uintptr_t)(a.maskA + ((size_t)bh * a.W + (w * NKBW + kb)) * Sp + q0);
+        const cu64* mp = (const cu64*)(uintptr_t)(a.maskA + ((size_t)bh * a.W + min(w * NKBW + kb, a.W - 1)) * Sp +
+                                                  keep_off(q0, Sp));
 #pragma unroll
         for (int i = 0; i < 16; ++i) mk[i] = mp[i];
       }

@@ -1,0 +1,329 @@
+// Plain projection GEMM for gfx950 (MI355X / CDNA4): one wave per SIMD, 128 x 128 per wave.
+//
+//   C[M, N] = A[M, K] . B[N, K]^T (+ bias[n])      EPI_STORE   (Linear forward, NT input gradient)
+//   C[M, N] += A[M, K] . B[N, K]^T                  EPI_ADD     (residual-branch input gradient)
+//
+// bf16 operands, fp32 accumulation, one bf16 rounding.  This is the delivery schedule of the
+// library kernel that ran these products before (hipBLASLt's stream-K MT256x256x64 kernel; its main
+// loop, disassembled from the shipped code object for study, is in profiles/r6_hipblaslt_sk3_mainloop.s),
+// re-derived for this framework's LDS image, tile order and epilogues:
+//
+// * 256-thread workgroup, one per CU (128 KiB of LDS), waves 2 (M) x 2 (N), each wave owns a
+//   128 x 128 output block = 8 x 8 tiles of v_mfma_f32_16x16x32_bf16 with its 256 fp32 accumulators in
+//   AGPRs (inline-asm MFMAs with "+a" operands: hipcc never moves them).  Per 64-deep K-step a wave
+//   issues 128 MFMAs against 32 ds_read_b128 and 16 LDS-DMA pieces -- a quarter of a fragment read per
+//   MFMA, where the 8-wave kernel of gemm.hip needs 3/8 and 8 barriers.
+// * A K-step's whole fragment set lives in VGPRs: R0 = the first 32 k (8 A + 8 B fragments), R1 = the
+//   second 32.  Phase 0 (MFMAs on R0) reads R1 from the current LDS buffer; once every wave has
+//   its R1 (barrier 1) the buffer is free and the 16 pieces of K-step s + 2 land in it by LDS-DMA
+//   (buffer_load_dwordx4 ... lds) while phase 0 continues.  Phase 1 (MFMAs on R1) waits for K-step
+//   s + 1's pieces (issued one K-step earlier; counted vmcnt), barrier 2, and reads the next R0.
+//   Two buffers therefore carry three K-steps in flight: registers, landed, landing.  Two barriers
+//   per K-step, and no MFMA ever waits on an LDS read issued less than ~10 MFMAs earlier.
+// * Persistent: one workgroup per CU walks its tiles in the XCD-aware order of gemm.hip (the 32
+//   workgroups of an XCD take consecutive tiles, so tiles in flight on an XCD share A panels).  The
+//   K-step stream runs straight across tiles: the last two K-steps of a tile prefetch the next
+//   tile's first two, so its epilogue runs while they land and nothing drains between tiles.
+// * LDS image: [row][64 k] rows of 128 B, 16-byte chunk index XOR (row & 7) (conflict-free
+//   ds_read_b128 and DMA writes; the DMA source address carries the swizzle).  The B rows are stored
+//   permuted (sigma below) so that after the MFMAs a lane holds 8 consecutive output columns per
+//   pair of tiles: the epilogue stores 16-byte vectors straight from the accumulators (a wave
+//   instruction covers 16 rows x 64 contiguous bytes), no LDS round trip.
+// * Bias: each wave DMAs the tile's bias row into its own 1 KiB LDS slot with the first K-step of
+//   the tile (older than every counted wait that follows, so it has landed by the epilogue).
+//
+// Shape contract (host-checked): M % 256 == 0, N % 256 == 0, K % 64 == 0, K >= 128, leading
+// dimensions % 8 == 0, 16-byte aligned bases.
+#include <type_traits>
+
+#include "common.h"
+
+using namespace dtd;
+
+namespace {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int BUF = 65536;            // one K-step: A [256][128 B] then B [256][128 B]
+constexpr int B_OFF = 32768;
+constexpr int BIAS_OFF = 2 * BUF;     // 4 x 1 KiB bias slots (one per wave)
+constexpr int LDS_BYTES = 2 * BUF + 4096;
+
+enum : int { EPI_STORE = 0, EPI_ADD = 3 };
+
+struct W4Args {
+  const bf16* a; const bf16* b; bf16* c; const bf16* bias;
+  int M, N, K, lda, ldb, ldc;
+};
+
+// ---- inline-asm building blocks (issue order = source order: every statement is volatile) ----
+__device__ __forceinline__ void mfma_acc(f32x4& c, const i32x4& b, const i32x4& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+}
+__device__ __forceinline__ void mfma_zero(f32x4& c, const i32x4& b, const i32x4& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
+}
+// LDS fragment read; the result is valid only after the matching s_waitcnt lgkmcnt
+template <int OFF>
+__device__ __forceinline__ void lds_rd(i32x4& d, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
+}
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+__device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+// 16-byte store with two wait states behind it.  Issued through the builtin, hipcc let a VALU write
+// (the next accumulator read) land on the store's data VGPRs in the very next instruction, and on
+// gfx950 the stored bytes then came out corrupted -- rows of zeros where the data registers were
+// reused (scripts/diag/w4_debug.py; any instruction between store and rewrite hid it).  In asm the
+// wait is part of the statement, so no schedule can put a write closer.
+__device__ __forceinline__ void store16(const i32x4& v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" :: "v"(v), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1, in order
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ int xcd_beg(int x, int ntiles) {
+  const int q = ntiles / 8, r = ntiles % 8;
+  return x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+}
+
+// LDS row l (0..255) of the B image holds weight row sigma(l): within each 128-row half (a wave
+// column), tile ni = (l >> 4) & 7, lane row i = l & 15 ->
+//   32 (ni >> 1) + 8 (i >> 2) + 4 (ni & 1) + (i & 3)
+// so the MFMA output of tiles 2j, 2j + 1 gives lane quad lq the columns 32 j + 8 lq + 0..7.
+// For a DMA piece p (rows 8p .. 8p + 7, lane row d = lane >> 3) this is piece_row(p) + 8 (d >> 2) + (d & 3).
+__host__ __device__ constexpr int b_piece_row(int p) {
+  return (p >> 4) * 128 + 32 * ((p >> 2) & 3) + 16 * (p & 1) + 4 * ((p >> 1) & 1);
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int li = lane & 15, lq = lane >> 4;
+  const int ntn = g.N / BN, ntiles = (g.M / BM) * ntn, nk = g.K / BK;
+  const int nwg = gridDim.x, x = blockIdx.x % 8, l = blockIdx.x / 8, per = nwg / 8;
+  const int beg = xcd_beg(x, ntiles), end = xcd_beg(x + 1, ntiles);
+  int t = beg + l;
+  if (t >= end) return;
+
+  const uint32_t lds0 = lds_addr(smem);
+  // ---- per-lane constants
+  const int d = lane >> 3, sc = ((lane & 7) ^ d) * 8;                 // DMA: lane row, swizzled chunk
+  const int vA = (d * g.lda + sc) * 2;
+  const int vB = ((8 * (d >> 2) + (d & 3)) * g.ldb + sc) * 2;
+  const uint32_t sw0 = ((lq ^ (li & 7)) * 16), sw1 = (((4 + lq) ^ (li & 7)) * 16);
+  const uint32_t rA0 = lds0 + (wm * 128 + li) * 128 + sw0, rA1 = lds0 + (wm * 128 + li) * 128 + sw1;
+  const uint32_t rB0 = lds0 + B_OFF + (wn * 128 + li) * 128 + sw0, rB1 = lds0 + B_OFF + (wn * 128 + li) * 128 + sw1;
+
+  // ---- DMA cursor: the K-step two ahead of the compute side
+  int dt = t, dkt = 0;
+  auto rsA_of = [&](int tt) { return rsrc(g.a + (size_t)(tt / ntn) * BM * g.lda, 0x7fffffff); };
+  auto rsB_of = [&](int tt) { return rsrc(g.b + (size_t)(tt % ntn) * BN * g.ldb, 0x7fffffff); };
+  auto dsA = rsA_of(dt), dsB = rsB_of(dt);
+  // one K-step's 16 pieces of the cursor into LDS buffer `buf`; then advance the cursor (past the
+  // last tile it keeps re-issuing a valid step: those pieces land in a buffer nothing reads again)
+  auto dma_piece = [&](int k, uint32_t buf) {
+    if (k < 8) {
+      const int p = w * 8 + k;
+      dma16(dsA, buf + p * 1024, vA, p * 8 * g.lda * 2 + dkt * 128);
+    } else {
+      const int p = w * 8 + (k - 8);
+      dma16(dsB, buf + B_OFF + p * 1024, vB, b_piece_row(p) * g.ldb * 2 + dkt * 128);
+    }
+  };
+  auto dma_advance = [&]() {
+    if (++dkt == nk) {
+      dkt = 0;
+      if (dt + per < end) {
+        dt += per;
+        dsA = rsA_of(dt);
+        dsB = rsB_of(dt);
+      }
+    }
+  };
+  const bool has_bias = EPI == EPI_STORE && g.bias != nullptr;
+  const auto rsBias = rsrc(g.bias, g.N * 2);   // out-of-range lanes read 0
+  auto dma_bias = [&](int tt) {
+    if (has_bias) dma16(rsBias, lds0 + BIAS_OFF + w * 1024, lane * 16, (tt % ntn) * BN * 2);
+  };
+
+  // ---- prologue: K-steps 0 and 1 (buffers 0, 1); R0 of K-step 0 (the first K-step DMAs the bias)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma_piece(k, lds0);
+  dma_advance();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma_piece(k, lds0 + BUF);
+  dma_advance();
+  wait_vm<16>();
+  barrier();
+
+  i32x4 fa0[8], fb0[8], fa1[8], fb1[8];
+  f32x4 acc[8][8];
+  static_for<0, 8>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    lds_rd<i * 2048>(fb0[i], rB0);
+  });
+  static_for<0, 8>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    lds_rd<i * 2048>(fa0[i], rA0);
+  });
+  wait_lgkm0();
+
+  int kt = 0;
+  uint32_t cur = 0;          // byte offset of the current K-step's buffer (0 / BUF)
+  bool after_epi = false;    // the previous step ran an epilogue (its stores sit in the vm queue)
+  int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+
+  while (true) {
+    const uint32_t nxt = cur ^ BUF;
+    // ---------------- phase 0: MFMAs on R0; read R1 (cur); barrier; DMA K-step s + 2 into cur
+    auto phase0 = [&](auto first_c) {
+      constexpr bool first = decltype(first_c)::value;
+      const uint32_t b1 = rB1 + cur, a1 = rA1 + cur;
+      static_for<0, 64>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, mi = i >> 3, ni = i & 7;
+        if constexpr (first) mfma_zero(acc[mi][ni], fb0[ni], fa0[mi]);
+        else mfma_acc(acc[mi][ni], fb0[ni], fa0[mi]);
+        if constexpr (i < 8) lds_rd<i * 2048>(fb1[i], b1);
+        else if constexpr (i < 16) lds_rd<(i - 8) * 2048>(fa1[i - 8], a1);
+        else if constexpr (i == 19) {
+          wait_lgkm0();
+          barrier();
+          if (kt == 0) dma_bias(t);   // the tile's bias, older than every later counted wait
+        } else if constexpr (i >= 20 && i < 52 && (i & 1) == 0) {
+          dma_piece((i - 20) >> 1, lds0 + cur);
+        }
+      });
+    };
+    if (kt == 0) phase0(std::true_type{});
+    else phase0(std::false_type{});
+    dma_advance();
+    // ---------------- phase 1: MFMAs on R1; K-step s + 1 landed (barrier 2); read R0 from nxt
+    const uint32_t b0n = rB0 + nxt, a0n = rA0 + nxt;
+    static_for<0, 64>([&](auto ic) {
+      constexpr int i = decltype(ic)::value, mi = i >> 3, ni = i & 7;
+      mfma_acc(acc[mi][ni], fb1[ni], fa1[mi]);
+      if constexpr (i == 7) {
+        // K-step s + 1 was issued one K-step ago; younger: this step's 16 pieces (+ the
+        // epilogue's stores / loads when the previous step ended a tile)
+        if (after_epi) wait_vm<(EPI == EPI_ADD ? 63 : 49)>();
+        else wait_vm<16>();
+        barrier();
+      } else if constexpr (i >= 8 && i < 40 && (i & 1) == 0) {
+        constexpr int k = (i - 8) >> 1;
+        if constexpr (k < 8) lds_rd<k * 2048>(fb0[k], b0n);
+        else lds_rd<(k - 8) * 2048>(fa0[k - 8], a0n);
+      }
+    });
+    wait_lgkm0();
+    after_epi = false;
+    cur = nxt;
+    if (++kt < nk) continue;
+
+    // ---------------- epilogue of tile t (the next tile's K-steps 0 and 1 are landing meanwhile)
+    // the asm MFMAs' results: wait out the last ones' passes before any accumulator read (hipcc
+    // does not know the asm statements are MFMAs); then one row of tiles at a time, each behind a
+    // fence that also orders it after the previous row's stores (live copies stay at 32 VGPRs)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    {
+      const auto rc = rsrc(g.c + (size_t)m0 * g.ldc + n0, 0x7fffffff);
+      const int vc = ((wm * 128 + li) * g.ldc + wn * 128 + 8 * lq) * 2;
+      bf16x8 b8[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        b8[j] = bf16x8{};
+        if (has_bias)
+          b8[j] = *reinterpret_cast<const bf16x8*>(smem + BIAS_OFF + w * 1024 + (wn * 128 + 32 * j + 8 * lq) * 2);
+      }
+      static_for<0, 8>([&](auto mic) {
+        constexpr int mi = decltype(mic)::value;
+        asm volatile("" : "+a"(acc[mi][0]), "+a"(acc[mi][1]), "+a"(acc[mi][2]), "+a"(acc[mi][3]),
+                     "+a"(acc[mi][4]), "+a"(acc[mi][5]), "+a"(acc[mi][6]), "+a"(acc[mi][7]) :: "memory");
+        i32x4 cin[4];
+        if constexpr (EPI == EPI_ADD) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            cin[j] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, vc, (mi * 16 * g.ldc + 32 * j) * 2, 0));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 lo = acc[mi][2 * j], hi = acc[mi][2 * j + 1];
+          float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const bf16x8 add8 = EPI == EPI_ADD ? __builtin_bit_cast(bf16x8, cin[j]) : b8[j];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)add8[e];
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+          store16(__builtin_bit_cast(i32x4, o), rc, vc, (mi * 16 * g.ldc + 32 * j) * 2);
+        }
+      });
+    }
+    t += per;
+    if (t >= end) break;
+    kt = 0;
+    after_epi = true;
+    m0 = (t / ntn) * BM;
+    n0 = (t % ntn) * BN;
+  }
+  // nothing may still write this workgroup's LDS when it ends (the cursor's trailing pieces)
+  wait_vm<0>();
+}
+
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || c < 8)
+      c = 256;
+    n = c;
+  }
+  return n;
+}
+
+}  // namespace
+
+DTD_EXPORT int dtd_gemm_w4_supported(int M, int N, int K) {
+  return M > 0 && N > 0 && K >= 2 * BK && M % BM == 0 && N % BN == 0 && K % BK == 0;
+}
+
+// epi: 0 = store (+ bias), 3 = add into c (no bias)
+DTD_EXPORT int dtd_gemm_w4(int epi, const void* a, int lda, const void* b, int ldb, void* c, int ldc, const void* bias,
+                           int M, int N, int K, hipStream_t s) {
+  if (!dtd_gemm_w4_supported(M, N, K)) return (int)hipErrorInvalidValue;
+  if ((lda | ldb | ldc) % 8 || lda < K || ldb < K || ldc < N) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)bias) % 16) return (int)hipErrorInvalidValue;
+  // every byte offset the kernel forms inside one A / B panel or C tile must fit 31 bits
+  if ((long long)BM * lda * 2 >= 0x7fffffffLL || (long long)BN * ldb * 2 >= 0x7fffffffLL ||
+      (long long)BM * ldc * 2 >= 0x7fffffffLL)
+    return (int)hipErrorInvalidValue;
+  if (epi != EPI_STORE && epi != EPI_ADD) return (int)hipErrorInvalidValue;
+  if (epi == EPI_ADD && bias) return (int)hipErrorInvalidValue;
+  W4Args g{(const bf16*)a, (const bf16*)b, (bf16*)c, (const bf16*)bias, M, N, K, lda, ldb, ldc};
+  const int ntiles = (M / BM) * (N / BN);
+  const int cus = num_cus() / 8 * 8;
+  const int nwg = ntiles >= cus ? cus : (ntiles + 7) / 8 * 8;
+  if (epi == EPI_STORE) hipLaunchKernelGGL(gemm_w4_kernel<EPI_STORE>, dim3(nwg), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(gemm_w4_kernel<EPI_ADD>, dim3(nwg), dim3(256), 0, s, g);
+  DTD_LAUNCH_CHECK();
+}

@@ -188,12 +188,57 @@ def gemm_f32_tn(a: torch.Tensor, b: torch.Tensor, splits: int | None = None) -> 
     return part
 
 
+# Plain bf16 products -- the Linear forward with bias, the NT input gradients, the residual-add input
+# gradient -- on the one-wave-per-SIMD kernel (ops/csrc/gemm_w4.hip: 128 x 128 per wave, whole K-step
+# fragment sets in registers, LDS-DMA into the buffer being drained, persistent across tiles).
+# DTD_GEMM_W4=0 keeps them on hipBLASLt.
+_W4 = [os.environ.get("DTD_GEMM_W4", "0") == "1"]
+
+
+def w4_enabled() -> bool:
+    return _ENABLED[0] and _W4[0]
+
+
+def set_w4(on: bool) -> None:
+    _W4[0] = bool(on)
+
+
+def w4_supported(M: int, N: int, K: int, *tensors) -> bool:
+    if not (all(_ok(t) for t in tensors) and _lib.has("dtd_gemm_w4")):
+        return False
+    return bool(_lib.lib().dtd_gemm_w4_supported(M, N, K))
+
+
+def gemm_w4(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """a . b^T (+ bias) on gemm_w4.hip; with ``out``: out += a . b^T in place (fp32 sum, one bf16
+    rounding; no bias)."""
+    M, K = a.shape
+    N = b.shape[0]
+    assert b.shape[1] == K, (a.shape, b.shape)
+    if out is None:
+        c = torch.empty((M, N), dtype=a.dtype, device=a.device)
+        epi = EPI_STORE
+    else:
+        assert out.shape == (M, N) and bias is None, (out.shape, bias is None)
+        c, epi = out, EPI_ADD
+    _lib.call("dtd_gemm_w4", epi, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+              _lib.ptr(bias), M, N, K, _lib.stream())
+    return c
+
+
+def _bias_ok(b) -> bool:
+    return b is None or (b.is_cuda and b.dtype == torch.bfloat16 and b.is_contiguous() and b.data_ptr() % 16 == 0)
+
+
 def linear_any(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
-    """F.linear, or a hand-written kernel: the fp32 one for fp32 operands, the bf16 one in the
-    all-native mode, when the shape tiles."""
+    """F.linear, or a hand-written kernel: the fp32 one for fp32 operands, the bf16 one-wave-per-SIMD
+    kernel (default) or the 8-wave one (all-native mode), when the shape tiles."""
     if (x.dtype == torch.float32 and x.dim() == 2 and f32_supported(x.shape[0], w.shape[0], x.shape[1], x, w)
             and (b is None or _ok1d32(b))):
         return gemm_f32_nt(x, w, b)
+    if (w4_enabled() and x.dim() == 2 and _bias_ok(b) and w4_supported(x.shape[0], w.shape[0], x.shape[1], x, w)):
+        return gemm_w4(x, w, b)
     if all_enabled() and x.dim() == 2 and supported(x.shape[0], w.shape[0], x.shape[1], x, w) and (
             b is None or (b.is_cuda and b.dtype == torch.bfloat16 and b.is_contiguous())):
         return linear(x, w, b)
@@ -471,6 +516,8 @@ def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     wt = transposed_for_dgrad(w)
     if wt is None:
         return dy @ w
+    if w4_enabled() and dy.dim() == 2 and w4_supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt):
+        return gemm_w4(dy, wt)
     if all_enabled() and dy.dim() == 2 and supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt):
         return matmul_nt(dy, wt)
     return torch.nn.functional.linear(dy, wt)
@@ -485,6 +532,8 @@ def dgrad_add_(c: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> torch.Tens
     wt = transposed_for_dgrad(w)
     if wt is None:
         return c.addmm_(dy, w)
+    if w4_enabled() and dy.dim() == 2 and w4_supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c):
+        return gemm_w4(dy, wt, out=c)
     if all_enabled() and dy.dim() == 2 and supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c):
         return matmul_nt_add_(c, dy, wt)
     return c.addmm_(dy, wt.t())

@@ -213,21 +213,27 @@ class GPipe(nn.Module):
     def local_value(self):  # torch Pipe returned an RRef; kept for script-level parity
         return self
 
-    def train_step(self, x: torch.Tensor, target: torch.Tensor, loss_fn, schedule: str = "1f1b") -> torch.Tensor:
-        """Forward + backward of one mini-batch; returns the loss (mean over micro-batches).
+    def train_step(self, x: torch.Tensor, target: torch.Tensor, loss_fn, schedule: str = "1f1b",
+                   loss_weighting: str = "tokens", ignore_index: int = -100) -> torch.Tensor:
+        """Forward + backward of one mini-batch; returns the mini-batch loss.
 
         ``1f1b``: after S-1 warm-up forwards, every new micro-batch forward is followed by the
         backward of the oldest one, so at most S micro-batches hold activations at a time
         (GPipe fill-drain keeps all ``chunks``, which is why torch Pipe checkpoints them).
         Backward of micro-batch m on stage s and forward of m+S-1 on stage 0 run on different
         devices and overlap.  ``gpipe``: all forwards, then all backwards.  The loss of each
-        micro-batch is ``loss_fn(out, target_chunk) / chunks`` (micro-batch mean)."""
+        micro-batch is ``loss_fn(out, target_chunk)`` weighted by its share of the batch's labelled
+        tokens (``loss_weighting="tokens"``: the loss of the concatenated batch, as ``forward`` +
+        one loss gives -- stage_pipeline.micro_loss_weights) or by 1 / chunks ("mean")."""
+        from .stage_pipeline import micro_loss_weights
         if schedule not in ("1f1b", "gpipe"):
             raise ValueError(schedule)
         mx = list(torch.chunk(x, self.chunks, dim=0))
         mt = list(torch.chunk(target, self.chunks, dim=0))
         n, S = len(mx), len(self.stages)
         pending, total = [], None
+        weights = (micro_loss_weights(target.to(self.devices[-1]), n, ignore_index) if loss_weighting == "tokens"
+                   else None)
 
         def fwd(m):
             h = mx[m]
@@ -235,7 +241,8 @@ class GPipe(nn.Module):
                 h = send_to(h, self.devices[s]) if torch.is_tensor(h) else h
                 with torch.cuda.device(self.devices[s]) if self.devices[s].type == "cuda" else _null():
                     h = self._run(s, m, h)
-            loss = loss_fn(h, mt[m].to(h.device)) / n
+            loss = loss_fn(h, mt[m].to(h.device))
+            loss = loss * weights[m].to(loss.device) if weights is not None else loss / n
             pending.append(loss)
             return loss.detach()
 

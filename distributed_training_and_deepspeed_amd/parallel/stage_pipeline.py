@@ -20,53 +20,90 @@ Schedules (``schedule``):
     The steady-state exchanges pair a send with the opposite receive in one
     ``batch_isend_irecv`` (both neighbours send at the same time there).
 
-The loss of micro-batch m is ``loss_fn(out_m, target_m) / chunks`` on the last stage, so the
-gradients are those of the mean of the micro-batch losses (torch Pipe + the reference's loss on
-the concatenated output give the same for equal micro-batches).
+The loss of micro-batch m is ``loss_fn(out_m, target_m)`` weighted by m's share of the batch's
+labelled (non-ignored) tokens, so the step's loss and gradients are those of ONE loss over the
+concatenated output, as the reference computes it (``loss_weighting="mean"``: the mean of the
+micro-batch means).  Receives are posted a micro-batch ahead and sends do not block; the
+``checkpoint`` option recomputes micro-batch forwards in the backward as torch Pipe does.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 from torch import nn
+from torch.utils.checkpoint import checkpoint as _ckpt
 
 from ..comm import logger as clog
 
 
+class _Recv:
+    """A posted receive: ``wait()`` returns the received activation on the stage's device."""
+
+    def __init__(self, work, buf, device, host: bool):
+        self.work, self.buf, self.device, self.host = work, buf, device, host
+
+    def wait(self) -> torch.Tensor:
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        return self.buf.to(self.device, non_blocking=True) if self.host else self.buf
+
+
 class _Link:
     """Point-to-point messages between neighbouring stages.  RCCL sends device tensors directly;
-    gloo (CPU tests, or several ranks sharing one GPU) stages device tensors through host memory."""
+    gloo (CPU tests, or several ranks sharing one GPU) stages device tensors through host memory.
+    Sends are non-blocking (``isend``; the handles are kept until ``drain``) and receives are
+    posted ahead of their consumer (``irecv``), so a stage computes while its next input is in
+    flight instead of blocking in ``recv``."""
 
     def __init__(self, group=None):
         self.group = group
         self.backend = dist.get_backend(group)
         self.rank = dist.get_rank(group)
+        self.inflight = []      # (work, tensor kept alive until the send completes)
 
     def _host(self, t: torch.Tensor) -> bool:
         return self.backend != "nccl" and t.is_cuda
 
-    def send(self, t: torch.Tensor, dst: int) -> None:
-        clog.send(t.cpu() if self._host(t) else t.contiguous(), dst, group=self.group)
+    def isend(self, t: torch.Tensor, dst: int) -> None:
+        t = t.detach()
+        t = t.cpu() if self._host(t) else t.contiguous()
+        self.inflight.append((clog.isend(t, dst, group=self.group), t))
 
-    def recv(self, like: torch.Tensor, src: int) -> torch.Tensor:
-        if self._host(like):
-            buf = torch.empty(like.shape, dtype=like.dtype)
-            clog.recv(buf, src, group=self.group)
-            return buf.to(like.device)
-        buf = torch.empty_like(like)
-        clog.recv(buf, src, group=self.group)
-        return buf
+    def irecv(self, like: torch.Tensor, src: int) -> _Recv:
+        host = self._host(like)
+        buf = torch.empty(like.shape, dtype=like.dtype) if host else torch.empty_like(like)
+        return _Recv(clog.irecv(buf, src, group=self.group), buf, like.device, host)
 
-    def send_recv(self, t: torch.Tensor, peer: int, like: torch.Tensor) -> torch.Tensor:
-        """Send ``t`` to ``peer`` and receive a ``like``-shaped tensor from it, posted together (the
-        peer does the same at the same time: two blocking sends would wait for each other)."""
+    def send_recv(self, t: torch.Tensor, peer: int, like: torch.Tensor) -> _Recv:
+        """Send ``t`` to ``peer`` and post the receive of a ``like``-shaped tensor from it in one
+        ``batch_isend_irecv`` (the peer does the same at the same time: two blocking sends would
+        wait for each other).  Only the receive is waited for, by its consumer."""
         host = self._host(t)
+        src = t.detach()
+        src = src.cpu() if host else src.contiguous()
         out = torch.empty(like.shape, dtype=like.dtype) if host else torch.empty_like(like)
-        ops = [dist.P2POp(dist.isend, t.cpu() if host else t.contiguous(), peer, self.group),
-               dist.P2POp(dist.irecv, out, peer, self.group)]
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-        return out.to(like.device) if host else out
+        ops = [dist.P2POp(dist.isend, src, peer, self.group), dist.P2POp(dist.irecv, out, peer, self.group)]
+        ws = dist.batch_isend_irecv(ops)
+        self.inflight.append((ws[0], src))
+        return _Recv(ws[1], out, like.device, host)
+
+    def drain(self) -> None:
+        for w, _ in self.inflight:
+            if w is not None:
+                w.wait()
+        self.inflight.clear()
+
+
+def micro_loss_weights(targets, chunks: int, ignore_index: int = -100):
+    """Per-micro-batch loss weights that make the micro-batch losses sum to the loss of the whole
+    concatenated batch: weight_m = (labelled tokens of m) / (labelled tokens of the batch), device
+    tensors (no host sync).  The reference computes ONE CrossEntropyLoss over the concatenated
+    pipeline output (/root/reference/model_parallel_training.py:68-75); with MLM labels (-100 on
+    ~85 % of the tokens) each micro-batch has a different labelled count, so the plain mean of
+    the micro-batch means would weight tokens unequally."""
+    counts = torch.stack([(t != ignore_index).sum() for t in torch.chunk(targets, chunks, dim=0)]).float()
+    return counts / counts.sum().clamp_min(1.0)
 
 
 class StagePipeline(nn.Module):
@@ -75,14 +112,25 @@ class StagePipeline(nn.Module):
 
     ``modules``: this stage's module sequence (already on ``device``).  ``act_shape(mb)``: shape
     of the activation passed between stages for a micro-batch of ``mb`` rows; ``act_dtype`` its
-    dtype.  ``loss_fn(out, target)``: the last stage's loss.  ``set_micro(m)`` (optional) keys
-    dropout masks on the micro-batch index, as the single-process GPipe does."""
+    dtype.  ``loss_fn(out, target)``: the last stage's (mean) loss.  ``loss_weighting``:
+    "tokens" (default: micro-batch m's mean loss weighted by its share of the batch's labelled
+    tokens, ``micro_loss_weights`` -- the loss and gradients of the whole concatenated batch) or
+    "mean" (the mean of the micro-batch means).  ``checkpoint``: activation recompute as torch
+    Pipe / ``parallel/pipeline.py`` -- "except_last" (every micro-batch but the last keeps only its
+    input and recomputes its forward in the backward), "always" or "never".  ``set_micro(m)``
+    (optional) keys dropout masks on the micro-batch index, so a recomputed forward draws the same
+    masks."""
 
     def __init__(self, modules, stage: int, num_stages: int, device, act_shape, act_dtype, loss_fn=None,
-                 chunks: int = 1, schedule: str = "gpipe", group=None, set_micro=None):
+                 chunks: int = 1, schedule: str = "gpipe", group=None, set_micro=None, checkpoint: str = "never",
+                 loss_weighting: str = "tokens", ignore_index: int = -100):
         super().__init__()
         if schedule not in ("gpipe", "1f1b"):
             raise ValueError(schedule)
+        if checkpoint not in ("never", "except_last", "always"):
+            raise ValueError(checkpoint)
+        if loss_weighting not in ("tokens", "mean"):
+            raise ValueError(loss_weighting)
         self.mods = nn.ModuleList(modules)
         self.stage, self.num_stages = stage, num_stages
         self.device = torch.device(device)
@@ -90,6 +138,8 @@ class StagePipeline(nn.Module):
         self.loss_fn = loss_fn
         self.chunks, self.schedule = chunks, schedule
         self.set_micro = set_micro
+        self.checkpoint = checkpoint
+        self.loss_weighting, self.ignore_index = loss_weighting, ignore_index
         self.link = _Link(group)
         self.first = stage == 0
         self.last = stage == num_stages - 1
@@ -101,6 +151,12 @@ class StagePipeline(nn.Module):
             x = mod(x)
         return x
 
+    def _run(self, m: int, x: torch.Tensor) -> torch.Tensor:
+        ck = self.checkpoint == "always" or (self.checkpoint == "except_last" and m < self.chunks - 1)
+        if ck and torch.is_grad_enabled() and self.training:
+            return _ckpt(lambda inp, _m=m: self._fwd(_m, inp), x, use_reentrant=False, preserve_rng_state=False)
+        return self._fwd(m, x)
+
     def _like(self, mb: int) -> torch.Tensor:
         return torch.empty(self.act_shape(mb), dtype=self.act_dtype, device=self.device)
 
@@ -109,7 +165,7 @@ class StagePipeline(nn.Module):
         """Forward + backward of one mini-batch on this stage.  ``inputs`` (stage 0: the token
         ids) and ``targets`` (last stage: the labels) may be None on the other stages, which then
         take the mini-batch size from ``rows``; the rows are split into ``chunks`` equal
-        micro-batches.  Returns the summed micro-batch losses on the last stage (detached), None
+        micro-batches.  Returns the mini-batch loss on the last stage (detached), None
         elsewhere."""
         n, S, s = self.chunks, self.num_stages, self.stage
         ref = inputs if inputs is not None else targets
@@ -118,6 +174,9 @@ class StagePipeline(nn.Module):
         mb = (ref.shape[0] if ref is not None else rows) // n
         mx = list(torch.chunk(inputs, n, dim=0)) if inputs is not None else [None] * n
         mt = list(torch.chunk(targets, n, dim=0)) if targets is not None else [None] * n
+        weights = None
+        if self.last and self.loss_weighting == "tokens":
+            weights = micro_loss_weights(targets.to(self.device), n, self.ignore_index)
         saved = []          # (input activation with grad, output or loss) per micro-batch in flight
         total = None
 
@@ -125,9 +184,10 @@ class StagePipeline(nn.Module):
             nonlocal total
             if x is not None and not self.first:
                 x = x.detach().requires_grad_(True)
-            y = self._fwd(m, mx[m] if self.first else x)
+            y = self._run(m, mx[m] if self.first else x)
             if self.last:
-                y = self.loss_fn(y, mt[m].to(self.device)) / n
+                y = self.loss_fn(y, mt[m].to(self.device))
+                y = y * weights[m] if weights is not None else y / n
                 total = y.detach() if total is None else total + y.detach()
             saved.append((x, y))
             return y
@@ -140,43 +200,61 @@ class StagePipeline(nn.Module):
                 y.backward(g)
             return None if self.first else x.grad
 
-        def recv_fwd():
-            return None if self.first else self.link.recv(self._like(mb), s - 1)
+        # receives are posted one micro-batch ahead of their consumer (double-buffered: the
+        # posted buffer and the one being consumed); every send is non-blocking
+        def post_fwd(m):
+            return None if self.first or m >= n else self.link.irecv(self._like(mb), s - 1)
+
+        def post_bwd(k):
+            return None if self.last or k >= n else self.link.irecv(self._like(mb), s + 1)
 
         def send_fwd(y):
             if not self.last:
-                self.link.send(y.detach(), s + 1)
-
-        def recv_bwd():
-            return None if self.last else self.link.recv(self._like(mb), s + 1)
+                self.link.isend(y, s + 1)
 
         def send_bwd(gx):
             if not self.first:
-                self.link.send(gx, s - 1)
+                self.link.isend(gx, s - 1)
+
+        def take(r):
+            return None if r is None else r.wait()
 
         if self.schedule == "gpipe":
+            nxt = post_fwd(0)
             for m in range(n):
-                send_fwd(forward(m, recv_fwd()))
-            for _ in range(n):
-                send_bwd(backward(recv_bwd()))
+                cur, nxt = nxt, post_fwd(m + 1)
+                send_fwd(forward(m, take(cur)))
+            nxt = post_bwd(0)
+            for k in range(n):
+                cur, nxt = nxt, post_bwd(k + 1)
+                send_bwd(backward(take(cur)))
         else:
             warm = min(S - s - 1, n)
+            nxt = post_fwd(0)
             for m in range(warm):
-                send_fwd(forward(m, recv_fwd()))
-            x = recv_fwd() if warm < n else None
+                cur, nxt = nxt, post_fwd(m + 1)
+                send_fwd(forward(m, take(cur)))
+            x = take(nxt) if warm < n else None
+            pend_x = None
             for i in range(n - warm):
+                if pend_x is not None:
+                    x = take(pend_x)
                 y = forward(warm + i, x)
                 # send this output, receive the gradient of the oldest in-flight micro-batch
-                g = None if self.last else self.link.send_recv(y.detach(), s + 1, self._like(mb))
+                g = None if self.last else take(self.link.send_recv(y.detach(), s + 1, self._like(mb)))
                 gx = backward(g)
                 if i == n - warm - 1:
                     send_bwd(gx)
+                    pend_x = None
                 elif self.first:
-                    x = None
+                    x, pend_x = None, None
                 else:
-                    x = self.link.send_recv(gx, s - 1, self._like(mb))
-            for _ in range(warm):
-                send_bwd(backward(recv_bwd()))
+                    pend_x = self.link.send_recv(gx, s - 1, self._like(mb))
+            nxt = post_bwd(0) if warm else None
+            for k in range(warm):
+                cur, nxt = nxt, post_bwd(k + 1) if k + 1 < warm else None
+                send_bwd(backward(take(cur)))
+        self.link.drain()
         if self.set_micro is not None:
             self.set_micro(0)
         return total

@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import gc
 import math
-import time
 import weakref
 
 import torch
@@ -35,18 +34,13 @@ def mlm_capacity(tokens: int, p: float = 0.15, sigmas: float = 8.0) -> int:
     return min(tokens, int(math.ceil(mean + sigmas * sd)) + 64)
 
 
-# ProcessGroupNCCL's watchdog thread polls the end events of enqueued collectives every 100 ms; one
-# that polls a warm-up collective while a (global-mode) capture runs gets "operation not permitted
-# when stream is capturing" and aborts the process (profiles/r5_capture_results.jsonl).  Collectives
-# issued during a capture are not enqueued to it, so once it has retired the (completed) warm-up
-# work it makes no HIP call until the capture ends.
-_WATCHDOG_DRAIN_S = 0.35
-
-
-def _drain_rccl_watchdog() -> None:
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-        time.sleep(_WATCHDOG_DRAIN_S)
+# Captures run with capture_error_mode="thread_local": only the capturing thread is barred from
+# capture-unsafe HIP calls.  ProcessGroupNCCL's watchdog thread polls the end events of enqueued
+# collectives (hipEventQuery) every 100 ms; under the default global mode one of those polls landing
+# inside the capture aborted the process ("operation not permitted when stream is capturing",
+# profiles/r5_capture_results.jsonl).  Work that other threads put on the capturing stream (the
+# autograd engine's backward, DDP's bucket all-reduces) is still captured: capture is per stream.
+CAPTURE_ERROR_MODE = "thread_local"
 
 
 class CapturedStep:
@@ -71,9 +65,8 @@ class CapturedStep:
                 self.warmup_losses.append(step_fn(**b))
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        _drain_rccl_watchdog()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode=CAPTURE_ERROR_MODE):
             self.out = step_fn(**self.static)
         self.warmup = len(batches)
         import torch.distributed as dist

@@ -213,9 +213,14 @@ def main_stage_per_process(args):
     chunks = args.micro_batch_count if args.pipeline else 1
     loss_fn = Fx.CrossEntropyLoss() if args.loss == "fused" else torch.nn.CrossEntropyLoss()
     upcast = args.loss != "fused"
+    ck = args.checkpoint
+    if ck == "auto":   # as the single-process form: recompute only where HBM is small
+        ck = "never" if not cuda or torch.cuda.get_device_properties(device).total_memory >= 64 * 2 ** 30 \
+            else "except_last"
     pipe = StagePipeline(mods, rank, world, device, act_shape=lambda mb: (mb, args.seq_len, config.hidden_size),
                          act_dtype=dtype, loss_fn=lambda out, t: loss_fn(_flat(out, upcast), t.reshape(-1)),
-                         chunks=chunks, schedule=args.schedule, set_micro=lambda m: setattr(owner.rt.rng, "micro", m))
+                         chunks=chunks, schedule=args.schedule, set_micro=lambda m: setattr(owner.rt.rng, "micro", m),
+                         checkpoint=ck if args.pipeline else "never")
     optimizer = torch_adamw([p for p in pipe.parameters() if p.requires_grad], lr=5e-5)
     dataset = load_synthetic(config, args.batch_size * args.training_steps, seq_len=args.seq_len, seed=0)
     g = torch.Generator().manual_seed(0)
@@ -259,7 +264,8 @@ def main_stage_per_process(args):
         torch.cuda.synchronize()
     comm.barrier()
     elapsed = time.time() - start
-    idle = owner.tracker.table(max(n, 1))[1 + rank][1] if graphed is None else 0.0
+    # a replayed graph has no host-side activity marks: its idle time is not measured
+    idle = owner.tracker.table(max(n, 1))[1 + rank][1] if graphed is None else None
     idle_all = [None] * world
     torch.distributed.all_gather_object(idle_all, idle)
     loss_all = [None] * world
@@ -267,7 +273,8 @@ def main_stage_per_process(args):
     if rank == 0:
         print(f"\nTotal Training Time: {elapsed:.2f} seconds")
         print("\nAverage Idle Time per Device:")
-        rows = [["Device", "Average Idle Time (ms)"]] + [[i, v] for i, v in enumerate(idle_all)]
+        rows = [["Device", "Average Idle Time (ms)"]] + [[i, "n/a (graph)" if v is None else v]
+                                                         for i, v in enumerate(idle_all)]
         try:
             from tabulate import tabulate
             print(tabulate(rows, headers="firstrow", floatfmt=".2f", tablefmt="fancy_grid"))
@@ -278,7 +285,8 @@ def main_stage_per_process(args):
                           "timed_steps": n, "graph": graphed is not None, "pipeline": args.pipeline,
                           "schedule": args.schedule if args.pipeline else None, "stages": world,
                           "mode": "stage-per-process", "transport": backend,
-                          "idle_ms_per_step": [round(v, 3) for v in idle_all],
+                          "checkpoint": ck if args.pipeline else None,
+                          "idle_ms_per_step": [None if v is None else round(v, 3) for v in idle_all],
                           "final_loss": loss_all[-1]}))
     comm.destroy()
 

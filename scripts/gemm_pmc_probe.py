@@ -46,12 +46,30 @@ def run_wgrad():
     print("ok", flush=True)
 
 
+def run_w4():
+    """gemm_w4.hip (one wave per SIMD) vs hipBLASLt on fc2 forward (N 768, K 3072) and o forward
+    (N 768, K 768) at T = 131072, three launches each."""
+    from distributed_training_and_deepspeed_amd.ops import gemm as G
+    from distributed_training_and_deepspeed_amd.utils.tuning import use_tuned_gemms
+    use_tuned_gemms()
+    T = 131072
+    for N, K in ((768, 3072), (768, 768)):
+        a = torch.rand(T, K, device="cuda", dtype=torch.bfloat16) * 2 - 1
+        b = torch.rand(N, K, device="cuda", dtype=torch.bfloat16) * 2 - 1
+        bias = torch.rand(N, device="cuda", dtype=torch.bfloat16)
+        for _ in range(3):
+            G.gemm_w4(a, b, bias)
+            torch.nn.functional.linear(a, b, bias)
+    torch.cuda.synchronize()
+    print("ok", flush=True)
+
+
 def summarize(paths):
     acc = defaultdict(lambda: defaultdict(list))
     for path in paths:
         for r in csv.DictReader(open(path)):
             name = r.get("Kernel_Name", "")
-            fam = ("ours" if ("gemm_bt" in name or "gemm_tn" in name or "wgrad_tn" in name)
+            fam = ("ours" if ("gemm_bt" in name or "gemm_tn" in name or "wgrad_tn" in name or "gemm_w4" in name)
                    else ("hipblaslt" if "Cijk" in name else None))
             if fam is None:
                 continue
@@ -67,5 +85,7 @@ if __name__ == "__main__":
         summarize(sys.argv[2:])
     elif len(sys.argv) > 1 and sys.argv[1] == "wgrad":
         run_wgrad()
+    elif len(sys.argv) > 1 and sys.argv[1] == "w4":
+        run_w4()
     else:
         run()

@@ -27,7 +27,8 @@ CASES = [
     (1, 200, 2, 64, True, True, 0.1),
     (1, 256, 2, 128, False, False, 0.0),
     (1, 160, 2, 128, True, False, 0.1),
-    (2, 64, 2, 64, False, False, 0.1),     # S < one 128-query tile: mask rows past W are over-read
+    (2, 64, 2, 64, False, False, 0.1),     # S < one 128-query tile: waves past W clamp their mask rows
+    (3, 96, 2, 64, False, False, 0.1),     # W = 3: the last key block's keep words clamp into the row
 ]
 
 
@@ -221,3 +222,23 @@ def test_f32_attention_kernels_match_fp64(B, S, H, D, causal, alibi, p):
     for i, name in enumerate("qkv"):
         e = rel(g[:, :, i], r[:, :, i])
         assert e < 5e-5, f"d{name} rel err {e}"
+
+
+@pytest.mark.parametrize("S", [64, 96, 512])
+def test_exact_size_mask_buffer(S):
+    """The keep-bit buffer is exactly 2 x mask_words (no read slack): fwd + bwd with dropout on it
+    match the reference, so every keep word the kernels use is inside it."""
+    B, H, D, p = 2, 3, 64, 0.1
+    masks = A.alloc_masks(B, H, S, torch.device("cuda"))
+    assert masks.untyped_storage().nbytes() == 2 * A.mask_words(B, H, S) * 4
+    torch.manual_seed(2)
+    qkv = torch.randn(B * S, 3 * H * D).to(torch.bfloat16)
+    dctx = torch.randn(B * S, H * D).to(torch.bfloat16)
+    rg, rc = RngState(13, device="cuda"), RngState(13, device="cpu")
+    ctx_g, lse_g, mk = A.attn_fwd(qkv.cuda(), B, S, H, D, False, None, p, rg, 3)
+    assert mk.untyped_storage().nbytes() == 2 * A.mask_words(B, H, S) * 4
+    ctx_r, lse_r = A.attn_fwd_ref(qkv, B, S, H, D, False, None, p, rc, 3)
+    assert rel(ctx_g, ctx_r) < 1e-2
+    dq_g = A.attn_bwd(dctx.cuda(), qkv.cuda(), ctx_g, lse_g, B, S, H, D, False, None, p, rg, 3, mk)
+    dq_r = A.attn_bwd_ref(dctx, qkv, ctx_r, lse_r, B, S, H, D, False, None, p, rc, 3)
+    assert rel(dq_g, dq_r) < 2e-2

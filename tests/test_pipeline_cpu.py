@@ -84,3 +84,32 @@ def test_1f1b_schedule_matches_gpipe_with_dropout():
     assert abs(res[0][0] - res[1][0]) < 1e-6
     for n in res[0][1]:
         assert torch.allclose(res[0][1][n], res[1][1][n], atol=1e-6), n
+
+
+def test_train_step_loss_equals_one_loss_over_the_concatenated_batch():
+    """train_step's token-weighted micro-batch losses give the loss and gradients of the reference's
+    single CrossEntropyLoss over the concatenated pipeline output (model_parallel_training.py:68-75),
+    with MLM labels whose labelled count differs per micro-batch."""
+    cfg = C.BERT_TINY
+    ds = SyntheticLMDataset(cfg, 8, seq_len=32, seed=1)
+    V = cfg.vocab_size
+
+    def loss_fn(out, t):
+        return torch.nn.functional.cross_entropy(out.reshape(-1, V).float(), t.reshape(-1))
+
+    counts = [int((t != -100).sum()) for t in torch.chunk(ds.labels, 4)]
+    assert len(set(counts)) > 1, counts
+    res = []
+    for mode in ("forward", "train_step"):
+        a = BertModelWithMP(cfg, devices=["cpu", "cpu"], impl="fused", seed=4)
+        a.train()
+        pipe = a.to_pipeline(chunks=4, checkpoint="never")
+        if mode == "forward":
+            loss = loss_fn(pipe(ds.input_ids), ds.labels)
+            loss.backward()
+        else:
+            loss = pipe.train_step(ds.input_ids, ds.labels, loss_fn, schedule="1f1b")
+        res.append((loss.item(), {n: p.grad.clone() for n, p in a.named_parameters() if p.grad is not None}))
+    assert abs(res[0][0] - res[1][0]) < 1e-5
+    for n in res[0][1]:
+        assert torch.allclose(res[0][1][n], res[1][1][n], atol=1e-6, rtol=1e-4), n
