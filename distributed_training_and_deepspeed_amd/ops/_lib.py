@@ -77,6 +77,7 @@ _SIGS = {
     "dtd_gemm_bt_supported": (I, [I, I, I]),
     # gemm_w4.hip
     "dtd_gemm_w4_supported": (I, [I, I, I]),
+    "dtd_gemm_w4_set_sched": (I, [I]),
     "dtd_gemm_w4": (I, [I, P, I, P, I, P, I, P, I, I, I, P]),
     "dtd_gemm_bt_part_rows": (I, [I]),
     "dtd_gemm_bt": (I, [I, P, I, P, I, P, I, P, P, I, P, P, I, I, I, P, P]),

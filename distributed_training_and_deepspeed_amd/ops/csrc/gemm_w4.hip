@@ -43,6 +43,7 @@ using namespace dtd;
 namespace {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int BUF = 65536;            // one K-step: A [256][128 B] then B [256][128 B]
@@ -51,6 +52,31 @@ constexpr int BIAS_OFF = 2 * BUF;     // 4 x 1 KiB bias slots (one per wave)
 constexpr int LDS_BYTES = 2 * BUF + 4096;
 
 enum : int { EPI_STORE = 0, EPI_ADD = 3 };
+
+// Schedule of one K-step (128 MFMA slots; side operations follow the MFMA of their slot):
+//   slots 0..15       R1 fragment reads (cur), one per MFMA
+//   slot  19          lgkmcnt(0) + barrier 1: cur is free
+//   slots 20 + 7k     the 16 LDS-DMA pieces of K-step s + 2 into cur, k = 0..15 (..125): spread
+//                     over the K-step so the 4 waves' pieces never queue at the texture unit
+//                     (a piece is 1 KiB; bunched 1 per 2 MFMAs they stalled the MFMA issue)
+//   slot  64 + B2I    vmcnt(pieces of this step issued so far) + barrier 2: K-step s + 1 landed
+//   slots 64+B2I+1+2k R0 fragment reads of K-step s + 1 (nxt), k = 0..15
+// (DMA0, DSTEP, B2I) is a template parameter set: SCHEDS lists the measured forms, SCHED_DEFAULT the
+// one that runs (dtd_gemm_w4_set_sched picks another for A/B runs, scripts/bench_gemm_w4.py).
+template <int DMA0, int DSTEP, int B2I>
+struct Sched {
+  static constexpr int dma0 = DMA0, dstep = DSTEP, b2i = B2I;
+  static constexpr int dma_slot(int k) { return DMA0 + DSTEP * k; }
+  static constexpr int pieces_before(int slot) {
+    int n = 0;
+    for (int k = 0; k < 16; ++k) n += dma_slot(k) < slot ? 1 : 0;
+    return n;
+  }
+  static constexpr int nb2 = pieces_before(64 + B2I);
+  static_assert(DMA0 > 19 && dma_slot(15) < 128 && nb2 < 16 && B2I + 31 < 64, "K-step schedule");
+};
+#define DTD_W4_SCHEDS(X) X(0, 20, 7, 24) X(1, 20, 6, 24) X(2, 20, 7, 16) X(3, 20, 6, 16) X(4, 20, 7, 28) X(5, 21, 7, 20)
+constexpr int SCHED_COUNT = 6, SCHED_DEFAULT = 0;
 
 struct W4Args {
   const bf16* a; const bf16* b; bf16* c; const bf16* bias;
@@ -82,6 +108,19 @@ __device__ __forceinline__ void store16(const i32x4& v, __amdgpu_buffer_rsrc_t r
   asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" :: "v"(v), "v"(voff), "s"(r), "s"(soff) : "memory");
 }
 
+// One LDS-DMA piece: 16 bytes per lane from rsrc + voff + soff to LDS address lds + 16 * lane.  M0 is
+// written here and not restored: no instruction hipcc emits in this kernel reads M0 (checked on the
+// ISA by tests/test_gemm_w4_asm_cpu.py), so the save / restore pair of common.h's dma16 is dropped
+// (2 SALU issues per piece, 32 per K-step).  The s_nop covers the M0-write -> LDS-DMA hazard.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma_lds(__amdgpu_buffer_rsrc_t r, uint32_t lds, int voff, int soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r), "s"(__builtin_amdgcn_readfirstlane(soff))
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 // compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1, in order
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -112,8 +151,9 @@ __host__ __device__ constexpr int b_piece_row(int p) {
   return (p >> 4) * 128 + 32 * ((p >> 2) & 3) + 16 * (p & 1) + 4 * ((p >> 1) & 1);
 }
 
-template <int EPI>
+template <int EPI, typename SC>
 __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
+  constexpr int B2I = SC::b2i, NB2 = SC::nb2;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -144,10 +184,10 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
   auto dma_piece = [&](int k, uint32_t buf) {
     if (k < 8) {
       const int p = w * 8 + k;
-      dma16(dsA, buf + p * 1024, vA, p * 8 * g.lda * 2 + dkt * 128);
+      dma_lds(dsA, buf + p * 1024, vA, p * 8 * g.lda * 2 + dkt * 128);
     } else {
       const int p = w * 8 + (k - 8);
-      dma16(dsB, buf + B_OFF + p * 1024, vB, b_piece_row(p) * g.ldb * 2 + dkt * 128);
+      dma_lds(dsB, buf + B_OFF + p * 1024, vB, b_piece_row(p) * g.ldb * 2 + dkt * 128);
     }
   };
   auto dma_advance = [&]() {
@@ -163,7 +203,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
   const bool has_bias = EPI == EPI_STORE && g.bias != nullptr;
   const auto rsBias = rsrc(g.bias, g.N * 2);   // out-of-range lanes read 0
   auto dma_bias = [&](int tt) {
-    if (has_bias) dma16(rsBias, lds0 + BIAS_OFF + w * 1024, lane * 16, (tt % ntn) * BN * 2);
+    if (has_bias) dma_lds(rsBias, lds0 + BIAS_OFF + w * 1024, lane * 16, (tt % ntn) * BN * 2);
   };
 
   // ---- prologue: K-steps 0 and 1 (buffers 0, 1); R0 of K-step 0 (the first K-step DMAs the bias)
@@ -188,6 +228,18 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
   });
   wait_lgkm0();
 
+  // EPI_ADD: the residual C tile is read in the epilogue; rows 0 and 1 of it are loaded during the
+  // tile's last K-step (older than that step's counted waits: landed by the epilogue) and each
+  // row's registers are refilled with row + 2 as the epilogue consumes them (4 rows in flight
+  // spilled the accumulators)
+  i32x4 cpre[2][4];
+  const int vc = ((wm * 128 + li) * g.ldc + wn * 128 + 8 * lq) * 2;
+  auto c_load = [&](__amdgpu_buffer_rsrc_t rc, int r, i32x4 (&dst)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      dst[j] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, vc, (r * 16 * g.ldc + 32 * j) * 2, 0));
+  };
+
   int kt = 0;
   uint32_t cur = 0;          // byte offset of the current K-step's buffer (0 / BUF)
   bool after_epi = false;    // the previous step ran an epilogue (its stores sit in the vm queue)
@@ -209,32 +261,46 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
           wait_lgkm0();
           barrier();
           if (kt == 0) dma_bias(t);   // the tile's bias, older than every later counted wait
-        } else if constexpr (i >= 20 && i < 52 && (i & 1) == 0) {
-          dma_piece((i - 20) >> 1, lds0 + cur);
+          if constexpr (EPI == EPI_ADD) {
+            if (kt == nk - 1) {
+              const auto rc = rsrc(g.c + (size_t)m0 * g.ldc + n0, 0x7fffffff);
+#pragma unroll
+              for (int r = 0; r < 2; ++r) c_load(rc, r, cpre[r]);
+            }
+          }
         }
+        static_for<0, 16>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          if constexpr (SC::dma_slot(k) == i) dma_piece(k, lds0 + cur);
+        });
       });
     };
     if (kt == 0) phase0(std::true_type{});
     else phase0(std::false_type{});
-    dma_advance();
     // ---------------- phase 1: MFMAs on R1; K-step s + 1 landed (barrier 2); read R0 from nxt
     const uint32_t b0n = rB0 + nxt, a0n = rA0 + nxt;
     static_for<0, 64>([&](auto ic) {
       constexpr int i = decltype(ic)::value, mi = i >> 3, ni = i & 7;
       mfma_acc(acc[mi][ni], fb1[ni], fa1[mi]);
-      if constexpr (i == 7) {
-        // K-step s + 1 was issued one K-step ago; younger: this step's 16 pieces (+ the
-        // epilogue's stores / loads when the previous step ended a tile)
-        if (after_epi) wait_vm<(EPI == EPI_ADD ? 63 : 49)>();
-        else wait_vm<16>();
+      if constexpr (i == B2I) {
+        // K-step s + 1 was issued one K-step ago; younger: the pieces of this step issued so far
+        // (+ the epilogue's stores / loads and the bias piece when the previous step ended a tile)
+        constexpr int after = NB2 + 1 + (EPI == EPI_ADD ? 56 : 32);   // ADD: 24 loads + 32 stores after the step
+        if (after_epi) wait_vm<(after > 63 ? 63 : after)>();
+        else wait_vm<NB2>();
         barrier();
-      } else if constexpr (i >= 8 && i < 40 && (i & 1) == 0) {
-        constexpr int k = (i - 8) >> 1;
+      } else if constexpr (i > B2I && i <= B2I + 31 && ((i - B2I) & 1) == 1) {
+        constexpr int k = (i - B2I - 1) >> 1;
         if constexpr (k < 8) lds_rd<k * 2048>(fb0[k], b0n);
         else lds_rd<(k - 8) * 2048>(fa0[k - 8], a0n);
       }
+      static_for<0, 16>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if constexpr (SC::dma_slot(k) == 64 + i) dma_piece(k, lds0 + cur);
+      });
     });
     wait_lgkm0();
+    dma_advance();
     after_epi = false;
     cur = nxt;
     if (++kt < nk) continue;
@@ -246,7 +312,6 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     {
       const auto rc = rsrc(g.c + (size_t)m0 * g.ldc + n0, 0x7fffffff);
-      const int vc = ((wm * 128 + li) * g.ldc + wn * 128 + 8 * lq) * 2;
       bf16x8 b8[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -261,20 +326,20 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
         i32x4 cin[4];
         if constexpr (EPI == EPI_ADD) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            cin[j] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, vc, (mi * 16 * g.ldc + 32 * j) * 2, 0));
+          for (int j = 0; j < 4; ++j) cin[j] = cpre[mi & 1][j];
+          if constexpr (mi < 6) c_load(rc, mi + 2, cpre[mi & 1]);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const f32x4 lo = acc[mi][2 * j], hi = acc[mi][2 * j + 1];
-          float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           const bf16x8 add8 = EPI == EPI_ADD ? __builtin_bit_cast(bf16x8, cin[j]) : b8[j];
+          i32x4 o;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += (float)add8[e];
-          bf16x8 o;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
-          store16(__builtin_bit_cast(i32x4, o), rc, vc, (mi * 16 * g.ldc + 32 * j) * 2);
+          for (int e = 0; e < 4; ++e)   // fp32 sum, one v_cvt_pk_bf16_f32 per pair
+            o[e] = __builtin_bit_cast(int, __builtin_convertvector(
+                       f32x2{v[2 * e] + (float)add8[2 * e], v[2 * e + 1] + (float)add8[2 * e + 1]}, bf16x2));
+          store16(o, rc, vc, (mi * 16 * g.ldc + 32 * j) * 2);
         }
       });
     }
@@ -303,6 +368,13 @@ int num_cus() {
 
 }  // namespace
 
+static int g_sched = SCHED_DEFAULT;
+DTD_EXPORT int dtd_gemm_w4_set_sched(int i) {
+  if (i < 0 || i >= SCHED_COUNT) return (int)hipErrorInvalidValue;
+  g_sched = i;
+  return 0;
+}
+
 DTD_EXPORT int dtd_gemm_w4_supported(int M, int N, int K) {
   return M > 0 && N > 0 && K >= 2 * BK && M % BM == 0 && N % BN == 0 && K % BK == 0;
 }
@@ -323,7 +395,17 @@ DTD_EXPORT int dtd_gemm_w4(int epi, const void* a, int lda, const void* b, int l
   const int ntiles = (M / BM) * (N / BN);
   const int cus = num_cus() / 8 * 8;
   const int nwg = ntiles >= cus ? cus : (ntiles + 7) / 8 * 8;
-  if (epi == EPI_STORE) hipLaunchKernelGGL(gemm_w4_kernel<EPI_STORE>, dim3(nwg), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL(gemm_w4_kernel<EPI_ADD>, dim3(nwg), dim3(256), 0, s, g);
+#define DTD_W4_LAUNCH(i, a0, st, b2)                                                                         \
+  case i:                                                                                                     \
+    if (epi == EPI_STORE)                                                                                     \
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI_STORE, Sched<a0, st, b2>>), dim3(nwg), dim3(256), 0, s, g);     \
+    else                                                                                                      \
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI_ADD, Sched<a0, st, b2>>), dim3(nwg), dim3(256), 0, s, g);       \
+    break;
+  switch (g_sched) {
+    DTD_W4_SCHEDS(DTD_W4_LAUNCH)
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef DTD_W4_LAUNCH
   DTD_LAUNCH_CHECK();
 }

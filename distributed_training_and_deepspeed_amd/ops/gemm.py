@@ -191,16 +191,21 @@ def gemm_f32_tn(a: torch.Tensor, b: torch.Tensor, splits: int | None = None) -> 
 # Plain bf16 products -- the Linear forward with bias, the NT input gradients, the residual-add input
 # gradient -- on the one-wave-per-SIMD kernel (ops/csrc/gemm_w4.hip: 128 x 128 per wave, whole K-step
 # fragment sets in registers, LDS-DMA into the buffer being drained, persistent across tiles).
-# DTD_GEMM_W4=0 keeps them on hipBLASLt.
-_W4 = [os.environ.get("DTD_GEMM_W4", "0") == "1"]
+# DTD_GEMM_W4=0 keeps them on hipBLASLt.  The residual-add form (EPI_ADD, the qkv input gradient) is
+# opt-in (DTD_GEMM_W4_ADD=1): its epilogue must read the C tile, and with one wave per SIMD that
+# read's latency is exposed (0.83x the library at T = 524288, profiles/r6_w4_sched.jsonl).
+_W4 = [os.environ.get("DTD_GEMM_W4", "1") == "1"]
+_W4_ADD = [os.environ.get("DTD_GEMM_W4_ADD", "0") == "1"]
 
 
 def w4_enabled() -> bool:
     return _ENABLED[0] and _W4[0]
 
 
-def set_w4(on: bool) -> None:
+def set_w4(on: bool, add: bool | None = None) -> None:
     _W4[0] = bool(on)
+    if add is not None:
+        _W4_ADD[0] = bool(add)
 
 
 def w4_supported(M: int, N: int, K: int, *tensors) -> bool:
@@ -532,7 +537,8 @@ def dgrad_add_(c: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> torch.Tens
     wt = transposed_for_dgrad(w)
     if wt is None:
         return c.addmm_(dy, w)
-    if w4_enabled() and dy.dim() == 2 and w4_supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c):
+    if (w4_enabled() and _W4_ADD[0] and dy.dim() == 2
+            and w4_supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c)):
         return gemm_w4(dy, wt, out=c)
     if all_enabled() and dy.dim() == 2 and supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c):
         return matmul_nt_add_(c, dy, wt)

@@ -63,18 +63,28 @@ def main():
     }
     if only:
         cases = {k: v for k, v in cases.items() if k in only.split(",")}
+    # SCHEDS="0,1,2": time gemm_w4.hip's K-step schedule variants (dtd_gemm_w4_set_sched) as extra columns
+    scheds = [int(x) for x in os.environ.get("SCHEDS", "").split(",") if x]
+    lib = __import__("distributed_training_and_deepspeed_amd.ops._lib", fromlist=["_lib"])
+
+    def sched(i, fn):
+        def run():
+            lib.call("dtd_gemm_w4_set_sched", i)
+            fn()
+            lib.call("dtd_gemm_w4_set_sched", 0)
+        return run
     fns = {}
     S = 2048
     for k, (a, bb, bias, add) in cases.items():
         fl = 2 * T * a.shape[1] * bb.shape[0]
         if add is None:
-            lib = (lambda a=a, bb=bb, bias=bias: L(a, bb, bias))
+            lib_fn = (lambda a=a, bb=bb, bias=bias: L(a, bb, bias))
             w4 = (lambda a=a, bb=bb, bias=bias: G.gemm_w4(a, bb, bias))
             w8 = (lambda a=a, bb=bb, bias=bias: G.gemm_bt(a, bb, bias))
             ref = a[:S].float() @ bb.float().t() + (bias.float() if bias is not None else 0)
             err = {"lib": rel(L(a[:S], bb, bias), ref), "w4": rel(G.gemm_w4(a[:S], bb, bias), ref)}
         else:
-            lib = (lambda a=a, bb=bb, add=add: add.addmm_(a, bb.t()))
+            lib_fn = (lambda a=a, bb=bb, add=add: add.addmm_(a, bb.t()))
             w4 = (lambda a=a, bb=bb, add=add: G.gemm_w4(a, bb, out=add))
             w8 = (lambda a=a, bb=bb, add=add: G.matmul_nt_add_(add, a, bb))
             c0 = add[:S].clone()
@@ -82,7 +92,10 @@ def main():
             c1 = c0.clone()
             G.gemm_w4(a[:S], bb, out=c1)
             err = {"lib": rel(c0.clone().addmm_(a[:S], bb.t()), ref), "w4": rel(c1, ref)}
-        fns[k] = (fl, {"lib": lib, "w4": w4, "w8": w8}, err)
+        row = {"lib": lib_fn, "w4": w4, "w8": w8}
+        for i in scheds:
+            row[f"w4s{i}"] = sched(i, w4)
+        fns[k] = (fl, row, err)
     for _, f, _ in fns.values():
         for fn in f.values():
             fn()
@@ -94,7 +107,7 @@ def main():
                 times[k][n].append(timed(fn, reps))
         print(json.dumps({"round": r}), flush=True)
     out = {}
-    tot = {"lib": 0.0, "w4": 0.0, "w8": 0.0}
+    tot = {n: 0.0 for n in next(iter(fns.values()))[1]}
     for k, (fl, f, err) in fns.items():
         row = {n: round(statistics.median(v), 1) for n, v in times[k].items()}
         for n in row:

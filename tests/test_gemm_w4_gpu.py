@@ -102,15 +102,15 @@ def test_w4_model_dispatch_matches_library():
     bias = torch.randn(3 * H, device="cuda").bfloat16()
     dy = torch.randn(T, 3 * H, device="cuda").bfloat16()
     res = torch.randn(T, H, device="cuda").bfloat16()
-    prev = G.w4_enabled()
+    prev = (G._W4[0], G._W4_ADD[0])
     try:
         outs = {}
         for on in (False, True):
-            G.set_w4(on)
+            G.set_w4(on, add=on)
             G.clear_transposes()
             r = res.clone()
             outs[on] = (G.linear_any(x, w, bias), G.dgrad(dy, w), G.dgrad_add_(r, dy, w))
         for lib_out, w4_out in zip(outs[False], outs[True]):
             assert rel(w4_out, lib_out) < 4e-3
     finally:
-        G.set_w4(prev)
+        G.set_w4(*prev)
