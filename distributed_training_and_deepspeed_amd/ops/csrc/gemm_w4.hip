@@ -75,8 +75,10 @@ struct Sched {
   static constexpr int nb2 = pieces_before(64 + B2I);
   static_assert(DMA0 > 19 && dma_slot(15) < 128 && nb2 < 16 && B2I + 31 < 64, "K-step schedule");
 };
-#define DTD_W4_SCHEDS(X) X(0, 20, 7, 24) X(1, 20, 6, 24) X(2, 20, 7, 16) X(3, 20, 6, 16) X(4, 20, 7, 28) X(5, 21, 7, 20)
-constexpr int SCHED_COUNT = 6, SCHED_DEFAULT = 0;
+// (the round-6 sweep over DMA0 20-21, DSTEP 6-7, B2I 16-30 measured all forms within 1 %,
+// profiles/r6_w4_sched.jsonl; two are kept)
+#define DTD_W4_SCHEDS(X) X(0, 20, 7, 24) X(1, 20, 6, 24)
+constexpr int SCHED_COUNT = 2, SCHED_DEFAULT = 0;
 
 struct W4Args {
   const bf16* a; const bf16* b; bf16* c; const bf16* bias;
@@ -120,6 +122,42 @@ __device__ __forceinline__ void dma_lds(__amdgpu_buffer_rsrc_t r, uint32_t lds, 
                : "memory", "m0");
 }
 #pragma clang diagnostic pop
+
+// 16-byte global load issued as asm (invisible to hipcc's wait-count pass, which would otherwise
+// wait vmcnt(0) -- for every DMA piece in flight -- at its first use); the result may be read only
+// after a counted wait that names it (wait_vm_pin) or one that provably retired it (pin_v4)
+__device__ __forceinline__ void load16(i32x4& d, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+__device__ __forceinline__ void pin_v4(i32x4 (&v)[4]) {
+  asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+}
+// The EPI_ADD prefetch of rows 0..2 (12 loads) as ONE asm statement executed at every K-step, whose
+// loads are skipped by a scalar branch inside the statement unless `go` (the tile's last K-step):
+// to hipcc the registers are written unconditionally every K-step, so their value never merges
+// across a branch or the loop edge -- where hipcc copied the conditionally loaded registers,
+// reading them before the data had landed (scripts/diag/audit_w4_asm.py).
+__device__ __forceinline__ void prefetch3(i32x4 (&c)[3][4], int go, __amdgpu_buffer_rsrc_t r, int voff, int s0,
+                                          int s1, int s2) {
+  asm volatile(
+      "s_cmp_eq_u32 %12, 0\n\ts_cbranch_scc1 .Lw4pf%=\n\t"
+      "buffer_load_dwordx4 %0, %13, %14, %15 offen\n\tbuffer_load_dwordx4 %1, %13, %14, %15 offen offset:64\n\t"
+      "buffer_load_dwordx4 %2, %13, %14, %15 offen offset:128\n\tbuffer_load_dwordx4 %3, %13, %14, %15 offen offset:192\n\t"
+      "buffer_load_dwordx4 %4, %13, %14, %16 offen\n\tbuffer_load_dwordx4 %5, %13, %14, %16 offen offset:64\n\t"
+      "buffer_load_dwordx4 %6, %13, %14, %16 offen offset:128\n\tbuffer_load_dwordx4 %7, %13, %14, %16 offen offset:192\n\t"
+      "buffer_load_dwordx4 %8, %13, %14, %17 offen\n\tbuffer_load_dwordx4 %9, %13, %14, %17 offen offset:64\n\t"
+      "buffer_load_dwordx4 %10, %13, %14, %17 offen offset:128\n\tbuffer_load_dwordx4 %11, %13, %14, %17 offen offset:192\n"
+      ".Lw4pf%=:"
+      : "=&v"(c[0][0]), "=&v"(c[0][1]), "=&v"(c[0][2]), "=&v"(c[0][3]), "=&v"(c[1][0]), "=&v"(c[1][1]),
+        "=&v"(c[1][2]), "=&v"(c[1][3]), "=&v"(c[2][0]), "=&v"(c[2][1]), "=&v"(c[2][2]), "=&v"(c[2][3])
+      : "s"(__builtin_amdgcn_readfirstlane(go)), "v"(voff), "s"(r), "s"(__builtin_amdgcn_readfirstlane(s0)),
+        "s"(__builtin_amdgcn_readfirstlane(s1)), "s"(__builtin_amdgcn_readfirstlane(s2))
+      : "memory", "scc");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_pin(i32x4 (&v)[4]) {
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : "n"(N) : "memory");
+}
 
 // compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1, in order
 template <int B, int E, typename F>
@@ -228,16 +266,17 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
   });
   wait_lgkm0();
 
-  // EPI_ADD: the residual C tile is read in the epilogue; rows 0 and 1 of it are loaded during the
-  // tile's last K-step (older than that step's counted waits: landed by the epilogue) and each
-  // row's registers are refilled with row + 2 as the epilogue consumes them (4 rows in flight
-  // spilled the accumulators)
-  i32x4 cpre[2][4];
+  // EPI_ADD reads the residual C tile in the epilogue (a row = this wave's 16 output rows x 128
+  // columns, 4 loads per lane).  Rows 0..2 are loaded during the tile's last K-step, before its DMA
+  // pieces, so that step's barrier-2 wait retires them; each row's registers are refilled with row
+  // + 3 as the epilogue consumes it, and rows 3..7 are waited for by count -- two rows of epilogue
+  // work cover each load.  The loads are asm (load16): issued through the builtin, hipcc waited
+  // vmcnt(0) at their first use, i.e. for every DMA piece of the next tile in flight.
+  i32x4 cpre[3][4];
   const int vc = ((wm * 128 + li) * g.ldc + wn * 128 + 8 * lq) * 2;
   auto c_load = [&](__amdgpu_buffer_rsrc_t rc, int r, i32x4 (&dst)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      dst[j] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, vc, (r * 16 * g.ldc + 32 * j) * 2, 0));
+    for (int j = 0; j < 4; ++j) load16(dst[j], rc, vc, (r * 16 * g.ldc + 32 * j) * 2);
   };
 
   int kt = 0;
@@ -262,11 +301,8 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
           barrier();
           if (kt == 0) dma_bias(t);   // the tile's bias, older than every later counted wait
           if constexpr (EPI == EPI_ADD) {
-            if (kt == nk - 1) {
-              const auto rc = rsrc(g.c + (size_t)m0 * g.ldc + n0, 0x7fffffff);
-#pragma unroll
-              for (int r = 0; r < 2; ++r) c_load(rc, r, cpre[r]);
-            }
+            const auto rc = rsrc(g.c + (size_t)m0 * g.ldc + n0, 0x7fffffff);
+            prefetch3(cpre, kt == nk - 1, rc, vc, 0, 16 * g.ldc * 2, 2 * 16 * g.ldc * 2);
           }
         }
         static_for<0, 16>([&](auto kc) {
@@ -285,7 +321,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
       if constexpr (i == B2I) {
         // K-step s + 1 was issued one K-step ago; younger: the pieces of this step issued so far
         // (+ the epilogue's stores / loads and the bias piece when the previous step ended a tile)
-        constexpr int after = NB2 + 1 + (EPI == EPI_ADD ? 56 : 32);   // ADD: 24 loads + 32 stores after the step
+        constexpr int after = NB2 + 1 + (EPI == EPI_ADD ? 52 : 32);   // ADD: 20 loads + 32 stores after the step
         if (after_epi) wait_vm<(after > 63 ? 63 : after)>();
         else wait_vm<NB2>();
         barrier();
@@ -310,6 +346,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
     // does not know the asm statements are MFMAs); then one row of tiles at a time, each behind a
     // fence that also orders it after the previous row's stores (live copies stay at 32 VGPRs)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    if constexpr (EPI == EPI_ADD) {
+      // rows 0..2 landed (retired by the last K-step's barrier-2 wait): no use may move above it
+#pragma unroll
+      for (int r = 0; r < 3; ++r) pin_v4(cpre[r]);
+    }
     {
       const auto rc = rsrc(g.c + (size_t)m0 * g.ldc + n0, 0x7fffffff);
       bf16x8 b8[4];
@@ -323,17 +364,16 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
         constexpr int mi = decltype(mic)::value;
         asm volatile("" : "+a"(acc[mi][0]), "+a"(acc[mi][1]), "+a"(acc[mi][2]), "+a"(acc[mi][3]),
                      "+a"(acc[mi][4]), "+a"(acc[mi][5]), "+a"(acc[mi][6]), "+a"(acc[mi][7]) :: "memory");
-        i32x4 cin[4];
-        if constexpr (EPI == EPI_ADD) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) cin[j] = cpre[mi & 1][j];
-          if constexpr (mi < 6) c_load(rc, mi + 2, cpre[mi & 1]);
+        if constexpr (EPI == EPI_ADD && mi >= 3) {
+          // row mi was loaded after row mi - 3's stores; younger since: the stores of rows mi-2,
+          // mi-1 and the loads of rows mi+1, mi+2 (those that exist)
+          wait_vm_pin<8 + 4 * ((mi + 1 <= 7) + (mi + 2 <= 7))>(cpre[mi % 3]);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const f32x4 lo = acc[mi][2 * j], hi = acc[mi][2 * j + 1];
           const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          const bf16x8 add8 = EPI == EPI_ADD ? __builtin_bit_cast(bf16x8, cin[j]) : b8[j];
+          const bf16x8 add8 = EPI == EPI_ADD ? __builtin_bit_cast(bf16x8, cpre[mi % 3][j]) : b8[j];
           i32x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e)   // fp32 sum, one v_cvt_pk_bf16_f32 per pair
@@ -341,6 +381,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(W4Args g) {
                        f32x2{v[2 * e] + (float)add8[2 * e], v[2 * e + 1] + (float)add8[2 * e + 1]}, bf16x2));
           store16(o, rc, vc, (mi * 16 * g.ldc + 32 * j) * 2);
         }
+        if constexpr (EPI == EPI_ADD && mi + 3 <= 7) c_load(rc, mi + 3, cpre[mi % 3]);
       });
     }
     t += per;

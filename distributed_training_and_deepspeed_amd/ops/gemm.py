@@ -194,8 +194,12 @@ def gemm_f32_tn(a: torch.Tensor, b: torch.Tensor, splits: int | None = None) -> 
 # DTD_GEMM_W4=0 keeps them on hipBLASLt.  The residual-add form (EPI_ADD, the qkv input gradient) is
 # opt-in (DTD_GEMM_W4_ADD=1): its epilogue must read the C tile, and with one wave per SIMD that
 # read's latency is exposed (0.83x the library at T = 524288, profiles/r6_w4_sched.jsonl).
+# The persistent grid is one workgroup per CU: with fewer than a few tiles per CU the tail and the
+# one-tile prologue dominate and hipBLASLt's smaller macro tiles fill the chip better, so the dispatch
+# takes the kernel only from DTD_GEMM_W4_MIN_TILES 256 x 256 tiles (default 4 per CU) up.
 _W4 = [os.environ.get("DTD_GEMM_W4", "1") == "1"]
 _W4_ADD = [os.environ.get("DTD_GEMM_W4_ADD", "0") == "1"]
+_W4_MIN_TILES = [int(os.environ.get("DTD_GEMM_W4_MIN_TILES", "0")) or None]
 
 
 def w4_enabled() -> bool:
@@ -212,6 +216,17 @@ def w4_supported(M: int, N: int, K: int, *tensors) -> bool:
     if not (all(_ok(t) for t in tensors) and _lib.has("dtd_gemm_w4")):
         return False
     return bool(_lib.lib().dtd_gemm_w4_supported(M, N, K))
+
+
+def w4_min_tiles() -> int:
+    if _W4_MIN_TILES[0] is None:
+        _W4_MIN_TILES[0] = 4 * torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return _W4_MIN_TILES[0]
+
+
+def _w4_pick(M: int, N: int, K: int, *tensors) -> bool:
+    """The dispatch rule: kernel on, shape tiles, and enough tiles to fill the persistent grid."""
+    return (w4_enabled() and (M // 256) * (N // 256) >= w4_min_tiles() and w4_supported(M, N, K, *tensors))
 
 
 def gemm_w4(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None,
@@ -242,7 +257,7 @@ def linear_any(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) 
     if (x.dtype == torch.float32 and x.dim() == 2 and f32_supported(x.shape[0], w.shape[0], x.shape[1], x, w)
             and (b is None or _ok1d32(b))):
         return gemm_f32_nt(x, w, b)
-    if (w4_enabled() and x.dim() == 2 and _bias_ok(b) and w4_supported(x.shape[0], w.shape[0], x.shape[1], x, w)):
+    if x.dim() == 2 and _bias_ok(b) and _w4_pick(x.shape[0], w.shape[0], x.shape[1], x, w):
         return gemm_w4(x, w, b)
     if all_enabled() and x.dim() == 2 and supported(x.shape[0], w.shape[0], x.shape[1], x, w) and (
             b is None or (b.is_cuda and b.dtype == torch.bfloat16 and b.is_contiguous())):
@@ -521,7 +536,7 @@ def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     wt = transposed_for_dgrad(w)
     if wt is None:
         return dy @ w
-    if w4_enabled() and dy.dim() == 2 and w4_supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt):
+    if dy.dim() == 2 and _w4_pick(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt):
         return gemm_w4(dy, wt)
     if all_enabled() and dy.dim() == 2 and supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt):
         return matmul_nt(dy, wt)
@@ -537,8 +552,7 @@ def dgrad_add_(c: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> torch.Tens
     wt = transposed_for_dgrad(w)
     if wt is None:
         return c.addmm_(dy, w)
-    if (w4_enabled() and _W4_ADD[0] and dy.dim() == 2
-            and w4_supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c)):
+    if _W4_ADD[0] and dy.dim() == 2 and _w4_pick(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c):
         return gemm_w4(dy, wt, out=c)
     if all_enabled() and dy.dim() == 2 and supported(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c):
         return matmul_nt_add_(c, dy, wt)

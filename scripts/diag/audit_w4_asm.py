@@ -9,7 +9,8 @@ properties of the emitted code that this script checks:
    ``... lds`` buffer load).
 2. LDS fragment reads: between a ``ds_read_b128`` issued by asm and the next ``s_waitcnt
    lgkmcnt``, no instruction other than an MFMA or another fragment read touches its destination
-   registers (a compiler copy there would read the registers before the data arrives).
+   registers (a compiler copy there would read the registers before the data arrives); likewise
+   no instruction touches an asm global load's registers before the next ``s_waitcnt vmcnt``.
 3. Epilogue stores: no instruction writes a ``buffer_store_dwordx4``'s data registers within two
    wait states of it (on gfx950 the store then wrote corrupted data: scripts/diag/w4_debug.py).
 4. MFMA results: scripts/diag/audit_mfma_hazards.py over the same kernels.
@@ -79,6 +80,20 @@ def audit_kernel(name, body):
                     continue
                 if _vregs(a) & dst:
                     probs.append(f"{name}: [{n}] ds_read {args} -> [{q}] {o} {a} before its lgkmcnt wait")
+                    break
+        # 2b. asm global loads (the EPI_ADD residual rows): untouched until a vmcnt wait
+        if op == "buffer_load_dwordx4" and from_asm[n] and "lds" not in args:
+            dst = _vregs(args.split(",")[0])
+            for q in range(n + 1, len(ins)):
+                o, a = ins[q]
+                if o == "s_waitcnt" and "vmcnt" in a:
+                    break
+                if o.startswith("s_"):
+                    continue
+                if o.startswith("buffer_load") and (from_asm[q] or not (_vregs(a.split(",")[0]) & dst)):
+                    continue   # another load: a later instance of the same asm prefetch (other code path)
+                if _vregs(a) & dst:
+                    probs.append(f"{name}: [{n}] {op} {args} -> [{q}] {o} {a} before a vmcnt wait")
                     break
         # 3. store data
         if op == "buffer_store_dwordx4":

@@ -94,15 +94,17 @@ def test_w4_strided_operands_and_output():
 
 
 def test_w4_model_dispatch_matches_library():
-    """linear_any / dgrad / dgrad_add_ with the kernel on vs hipBLASLt, same inputs."""
+    """linear_any / dgrad / dgrad_add_ with the kernel on vs hipBLASLt, same inputs (T large enough
+    for every product to pass the tile-count rule, which is checked too)."""
     torch.manual_seed(4)
-    T = 4096
+    T = 256 * 1024
     x = torch.randn(T, H, device="cuda").bfloat16()
     w = (torch.randn(3 * H, H, device="cuda") * 0.05).bfloat16()
     bias = torch.randn(3 * H, device="cuda").bfloat16()
     dy = torch.randn(T, 3 * H, device="cuda").bfloat16()
     res = torch.randn(T, H, device="cuda").bfloat16()
     prev = (G._W4[0], G._W4_ADD[0])
+    assert (T // 256) * (H // 256) >= G.w4_min_tiles()
     try:
         outs = {}
         for on in (False, True):
@@ -114,3 +116,11 @@ def test_w4_model_dispatch_matches_library():
             assert rel(w4_out, lib_out) < 4e-3
     finally:
         G.set_w4(*prev)
+
+
+def test_w4_dispatch_tile_rule():
+    """Small products (the b4 step's 2048 tokens) stay on the library, large ones take the kernel."""
+    n = G.w4_min_tiles()
+    assert G.w4_supported(2048, 768, 768) and not G._w4_pick(2048, 768, 768)
+    m = 256 * ((n + 2) // 3)
+    assert G._w4_pick(m, 768, 768) == G.w4_enabled()

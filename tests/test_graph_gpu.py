@@ -166,14 +166,17 @@ def test_captured_step_with_rccl_collectives_matches_eager(engine):
     scripts/diag/capture_collectives.py side_stream_rs) and defers their waits to the readers of
     the results, so in the graph each collective is a branch parallel to the following backward.
 
-    Each case runs in a fresh process, as a training process owns one process group: in one
-    pytest process, after the captured ZeRO tests above (each creating and destroying its own
-    group), the first replay of this DDP graph segfaulted inside hipGraphLaunch although the case
-    passes alone (profiles/r5_capture_results.jsonl)."""
+    The cases run in THIS process, after the captured ZeRO tests above (each creating and
+    destroying its own RCCL group): that sequence is the regression test of the round-5 crash, a
+    segfault in hipGraphLaunch on the first replay of the DDP graph.  Its cause was in the HIP
+    runtime's multi-queue graph replay (hip::Graph::UpdateStreams read past its parallel-stream
+    list when those streams shared the launch stream's hardware queue); the framework replays
+    graphs on one queue (DEBUG_HIP_FORCE_GRAPH_QUEUES=1, set at package import and in conftest.py).
+    DTD_RCCL_CAPTURE_INPROC=0 runs each case in a fresh process instead."""
     import os
     import subprocess
     import sys
-    if os.environ.get("DTD_RCCL_CAPTURE_INPROC") == "1":   # diagnosis: in this process
+    if os.environ.get("DTD_RCCL_CAPTURE_INPROC", "1") == "1":
         os.environ["MASTER_PORT"] = str(32000 + os.getpid() % 1000 + len(engine))
         _rccl_capture_case(engine)
         return
