@@ -441,12 +441,25 @@ def transpose(w: torch.Tensor) -> torch.Tensor:
 _DGRAD_NT = [os.environ.get("DTD_DGRAD_NT", "1") == "1"]
 
 
-def transposed_for_dgrad(w: torch.Tensor) -> torch.Tensor | None:
-    """W^T contiguous for the NT input-gradient form, or None (keep dy @ W)."""
+# A fresh transpose moves 4 bytes per weight element; the input-gradient GEMM does 2 * rows flops per
+# element.  With few rows (a micro-batch of 512 tokens on a ZeRO-3-gathered weight, whose transpose
+# cannot be prepared ahead) the transpose costs more than the NT form saves -- 11 ms of a 165 ms
+# step on the 16 B-parameter ZeRO-3 model (profiles/r6_mp3_step_window.txt) -- so below this many
+# rows an uncached weight keeps the NN form (dy @ W).
+_DGRAD_NT_MIN_ROWS = int(os.environ.get("DTD_DGRAD_NT_MIN_ROWS", "8192"))
+
+
+def transposed_for_dgrad(w: torch.Tensor, rows: int | None = None) -> torch.Tensor | None:
+    """W^T contiguous for the NT input-gradient form, or None (keep dy @ W).  ``rows``: the
+    gradient's row count, for the fresh-transpose cost rule above."""
     if not (_DGRAD_NT[0] and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()):
         return None
     if w.shape[0] % 8:   # W^T rows (the GEMM's K) would not be 16-byte aligned (e.g. a 28996-row vocabulary)
         return None
+    if rows is not None and rows < _DGRAD_NT_MIN_ROWS:
+        e = _WT_CACHE.get(id(w))
+        if not (e is not None and e[0] is w and e[1] == w.data_ptr()):
+            return None
     return transposed(w)
 
 
@@ -533,7 +546,7 @@ def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
             and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w)):
         wt = _t32(w)
         return gemm_f32_nn(dy, w) if wt is None or _F32_DGRAD_NN else gemm_f32_nt(dy, wt)
-    wt = transposed_for_dgrad(w)
+    wt = transposed_for_dgrad(w, dy.shape[0] if dy.dim() == 2 else None)
     if wt is None:
         return dy @ w
     if dy.dim() == 2 and _w4_pick(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt):
@@ -549,7 +562,7 @@ def dgrad_add_(c: torch.Tensor, dy: torch.Tensor, w: torch.Tensor) -> torch.Tens
             and f32_supported(dy.shape[0], w.shape[1], dy.shape[1], dy, w, c)):
         wt = _t32(w)
         return gemm_f32_nn(dy, w, out=c) if wt is None or _F32_DGRAD_NN else gemm_f32_nt(dy, wt, out=c)
-    wt = transposed_for_dgrad(w)
+    wt = transposed_for_dgrad(w, dy.shape[0] if dy.dim() == 2 else None)
     if wt is None:
         return c.addmm_(dy, w)
     if _W4_ADD[0] and dy.dim() == 2 and _w4_pick(dy.shape[0], wt.shape[0], dy.shape[1], dy, wt, c):
