@@ -94,11 +94,15 @@ def parse():
                          "device or 4 MB pinned host buffer RCCL's init allocates)")
     ap.add_argument("--ddp-overlap", default="on", choices=["on", "off"],
                     help="diagnostic: off launches every bucket collective after the backward")
-    ap.add_argument("--prewarm", default="auto", choices=["auto", "none", "layer1", "layer1-batch", "tiny", "full"],
+    ap.add_argument("--prewarm", default="auto", choices=["auto", "none", "layer1", "layer1-batch", "tiny", "full",
+                                                          "blas", "reserve", "custom"],
                     help="one forward+backward of a throwaway copy of the model before the RCCL group is "
                          "created (auto: a 1-layer copy at batch 1 whenever a group is created; layer1-batch: "
                          "1 layer at the bench batch; tiny: full depth, batch 1; full: full depth at the bench "
-                         "batch; utils/prewarm.py)")
+                         "batch; utils/prewarm.py).  Bisect arms: blas (one hipBLASLt GEMM only), reserve (only "
+                         "an allocator reservation of --reserve-gb), custom (the 1-layer step with the products "
+                         "on the hand-written GEMMs, no hipBLASLt where they tile)")
+    ap.add_argument("--reserve-gb", type=float, default=48.0, help="--prewarm reserve: bytes to reserve")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--no-tuned-gemms", action="store_true", help="skip the measured hipBLASLt solution table")
     return ap.parse_args()
@@ -128,7 +132,13 @@ def main():
             tuned = use_tuned_gemms()
     device = torch.device("cuda", local) if cuda else torch.device("cpu")
     group = world > 1 or args.zero_stage is not None or args.force_collectives or args.comm_init != "none"
-    if cuda and args.prewarm != "none" and (args.prewarm != "auto" or (group and prewarm_enabled())):
+    if cuda and args.prewarm in ("blas", "reserve"):
+        from distributed_training_and_deepspeed_amd.utils.prewarm import prewarm_blas, prewarm_reserve
+        if args.prewarm == "blas":
+            prewarm_blas(device)
+        else:
+            prewarm_reserve(device, int(args.reserve_gb * 1e9))
+    elif cuda and args.prewarm != "none" and (args.prewarm != "auto" or (group and prewarm_enabled())):
         # the step's kernels run once before the RCCL communicator exists (utils/prewarm.py:
         # kernels first launched after it run 5-25 % slower for the life of the process)
         prewarm_model_kernels(args.model, device, dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32,
@@ -136,6 +146,7 @@ def main():
                               layers=None if args.prewarm in ("tiny", "full") else 1,
                               batch=args.batch_size if args.prewarm in ("full", "layer1-batch") else 1,
                               static_mlm=not args.dense_mlm_head and args.mlm_capacity == "static",
+                              library_gemms=args.prewarm != "custom",
                               **({"sparse_mlm_head": not args.dense_mlm_head} if get_config(args.model).family == "bert" else {}))
     probe = None
     real_group = world > 1 or args.zero_stage is not None or args.force_collectives   # ZeRO always runs on a group
@@ -314,7 +325,7 @@ def main():
                 "tuned_gemms": tuned,
                 "hip_graph": graphed is not None,
                 "force_collectives": args.force_collectives,
-                "post_init_kernel_probe": post_init,
+                "post_init_kernel_probe": post_init, "prewarm": args.prewarm,
                 "async_wgrad": args.async_wgrad == "on",
                 "opt_overlap": opt_overlap,
                 "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if cuda else None,

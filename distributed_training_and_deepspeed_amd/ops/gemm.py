@@ -27,6 +27,7 @@ the elementwise kernels otherwise.  bf16 only.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -222,6 +223,21 @@ def w4_min_tiles() -> int:
     if _W4_MIN_TILES[0] is None:
         _W4_MIN_TILES[0] = 4 * torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
     return _W4_MIN_TILES[0]
+
+
+@contextlib.contextmanager
+def hand_kernels_at_any_size(library: bool = True):
+    """Within the block the one-wave-per-SIMD kernel takes every product it tiles, whatever its
+    tile count (and with ``library=False`` the 8-wave kernel the rest it tiles): the prewarm's
+    batch-1 step (utils/prewarm.py) then launches the kernels the real step will use."""
+    prev = (_W4_MIN_TILES[0], _ALL[0])
+    _W4_MIN_TILES[0] = 1
+    if not library:
+        _ALL[0] = True
+    try:
+        yield
+    finally:
+        _W4_MIN_TILES[0], _ALL[0] = prev
 
 
 def _w4_pick(M: int, N: int, K: int, *tensors) -> bool:

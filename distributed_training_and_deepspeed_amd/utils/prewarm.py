@@ -26,7 +26,35 @@ def prewarm_enabled() -> bool:
 
 def prewarm_model_kernels(name: str, device, dtype=torch.bfloat16, impl: str = "auto", seq_len: int = 512,
                           layers: int | None = 1, batch: int = 1, static_mlm: bool = True, optimizer: bool = True,
-                          **model_kw) -> None:
+                          library_gemms: bool = True, **model_kw) -> None:
+    """``library_gemms=False``: the products the hand-written GEMMs tile run on them instead of
+    hipBLASLt (the "custom kernels only" arm of the bisect, bench.py --prewarm custom).  Either
+    way the one-wave-per-SIMD GEMM takes the batch-1 products (it would not at that size in a
+    real step) so that the kernel the big step uses is launched here."""
+    from ..ops import gemm as G
+    with G.hand_kernels_at_any_size(library=library_gemms):
+        _prewarm(name, device, dtype, impl, seq_len, layers, batch, static_mlm, optimizer, **model_kw)
+
+
+def prewarm_blas(device, dtype=torch.bfloat16, m: int = 4096, n: int = 768, k: int = 768) -> None:
+    """Bisect arm: only a hipBLASLt handle / workspace and one GEMM (with bias, the forward form)."""
+    a = torch.randn(m, k, device=device, dtype=dtype)
+    w = torch.randn(n, k, device=device, dtype=dtype)
+    b = torch.randn(n, device=device, dtype=dtype)
+    torch.nn.functional.linear(a, w, b)
+    torch.cuda.synchronize(device)
+
+
+def prewarm_reserve(device, nbytes: int) -> None:
+    """Bisect arm: only the caching allocator's reservation of ``nbytes`` (the step's peak), freed
+    to the cache (not to the driver) so the step's tensors are carved from it."""
+    t = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    t.fill_(0)
+    torch.cuda.synchronize(device)
+    del t
+
+
+def _prewarm(name, device, dtype, impl, seq_len, layers, batch, static_mlm, optimizer, **model_kw) -> None:
     from ..data import SyntheticLMDataset
     from ..models import get_config
     from ..models.bert import BertForMaskedLM
