@@ -148,11 +148,7 @@ def main():
                               static_mlm=not args.dense_mlm_head and args.mlm_capacity == "static",
                               library_gemms=args.prewarm != "custom",
                               **({"sparse_mlm_head": not args.dense_mlm_head} if get_config(args.model).family == "bert" else {}))
-    probe = None
     real_group = world > 1 or args.zero_stage is not None or args.force_collectives   # ZeRO always runs on a group
-    if cuda and real_group:
-        from distributed_training_and_deepspeed_amd.utils.prewarm import KernelProbe
-        probe = KernelProbe(device)   # probe kernel 0 runs before the communicator exists
     if real_group:
         comm.init(rank=rank, world_size=world, local_rank=local)
     elif args.comm_init != "none":   # diagnostic process-group / allocation forms (world 1 only)
@@ -179,11 +175,6 @@ def main():
         else:
             dist.init_process_group(backend="nccl" if args.comm_init == "rccl-lazy" else "gloo", rank=rank,
                                     world_size=world)
-    post_init = probe.measure() if probe is not None else None
-    if post_init is not None and post_init["ratio"] > 1.05:
-        print(f"[dtd] WARNING: a kernel first launched after comm.init runs {post_init['ratio']:.3f}x slower "
-              "than its twin launched before it: kernels the prewarm did not cover may be slow in this "
-              "process (utils/prewarm.py, ops/csrc/probe.hip)", file=sys.stderr)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     cfg = get_config(args.model)
     mlm = cfg.family == "bert"
@@ -325,7 +316,7 @@ def main():
                 "tuned_gemms": tuned,
                 "hip_graph": graphed is not None,
                 "force_collectives": args.force_collectives,
-                "post_init_kernel_probe": post_init, "prewarm": args.prewarm,
+                "prewarm": args.prewarm,
                 "async_wgrad": args.async_wgrad == "on",
                 "opt_overlap": opt_overlap,
                 "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if cuda else None,

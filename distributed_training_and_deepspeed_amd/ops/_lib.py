@@ -103,9 +103,6 @@ _SIGS = {
     "dtd_gemm_ln": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, F, P, U32, P]),
     # reduce.hip
     "dtd_splitk_reduce": (I, [P, I, I, ctypes.c_longlong, P, I, I, P]),
-    # probe.hip, probe_post.hip
-    "dtd_probe": (I, [P, P, SZ, I, P]),
-    "dtd_probe_post": (I, [P, P, SZ, I, P]),
 }
 
 

@@ -11,7 +11,16 @@ Loading the code objects, torch's stream pools or a few GEMMs first does not hel
 
 ``prewarm_model_kernels`` builds a throwaway copy of the model (``layers`` deep -- every encoder
 layer runs the same kernels), runs one batch-1 forward + backward on synthetic tokens and frees
-it (and one fused Adam step on its gradients).  The entry scripts call it before ``comm.init`` (env ``DTD_PREWARM=0`` turns it off)."""
+it (and one fused Adam step on its gradients).  The entry scripts call it before ``comm.init`` (env ``DTD_PREWARM=0`` turns it off).
+
+Round-6 bisect (profiles/r6_prewarm_bisect.jsonl: b256 with RCCL bucket all-reduces at world 1,
+two interleaved rounds, fresh processes): no prewarm 1.315 / 1.321 M tokens/s; one hipBLASLt
+GEMM only (``prewarm_blas``) 1.318 / 1.317 M; a 45 GB allocator reservation only
+(``prewarm_reserve``) 1.315 / 1.314 M; the 1-layer step with its products on the hand-written
+kernels (hipBLASLt only where they do not tile) 1.459 / 1.462 M; the default prewarm 1.461 /
+1.461 M.  So the part that matters is the first launch of the framework's own kernels before the
+communicator exists -- not the BLAS handle, not the allocator.  The round-5 post-init probe (a
+streaming kernel pair in its own code object) never fired and was removed."""
 from __future__ import annotations
 
 import dataclasses
@@ -90,63 +99,3 @@ def _prewarm(name, device, dtype, impl, seq_len, layers, batch, static_mlm, opti
     if dev.type == "cuda":
         torch.cuda.empty_cache()   # hand the throwaway model's memory back (large ZeRO-3 runs)
     torch.random.set_rng_state(rng_state)
-
-
-class KernelProbe:
-    """Per-run check of the generic form of the post-communicator slowdown (ops/csrc/probe.hip):
-    build one BEFORE ``comm.init`` (it launches probe kernel 0) and call ``measure()`` after it --
-    probe kernel 1, code-identical but in its own code object (probe_post.hip), is first launched
-    then, on buffers allocated then; both stream a buffer through HBM, the kind of kernel round 4
-    saw hit (split-K reduce and column-sum finalize 3x, profiles/r4_s38_rccl_init_kernels.txt),
-    and are timed back to back.  ``ratio`` > 1.05 means kernels first used after the communicator
-    exists run slower in this process.  Round 5 measured 0.98-1.03 with and without the prewarm
-    while the step without it was 9 % slower (profiles/r5_s36_post_init_probe.jsonl): the slowdown
-    is tied to state the prewarm step creates, not to kernel first launch or allocation order."""
-
-    NUMEL, BLOCKS = 16 << 20, 2048     # 64 MiB in, 64 MiB out
-
-    def __init__(self, device):
-        from ..ops import _lib
-        self._lib = _lib
-        self.x = torch.ones(self.NUMEL, dtype=torch.float32, device=device)
-        self.y = torch.empty_like(self.x)
-        for _ in range(3):
-            self._run(0)
-        torch.cuda.synchronize()
-
-    def _run(self, i: int, blocks: int | None = None, n: int | None = None) -> None:
-        x, y = (self.x2, self.y2) if i else (self.x, self.y)
-        self._lib.call("dtd_probe_post" if i else "dtd_probe", x.data_ptr(), y.data_ptr(),
-                       n or self.NUMEL, blocks or self.BLOCKS, self._lib.stream())
-
-    def _time(self, i: int, reps: int = 5, blocks: int | None = None, n: int | None = None) -> float:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            self._run(i, blocks, n)
-        e1.record()
-        e1.synchronize()
-        return e0.elapsed_time(e1) / reps * 1e3
-
-    def measure(self, rounds: int = 7) -> dict:
-        """Two forms per twin, interleaved: the 128 MiB stream (~25 us) and a small one (256 KiB,
-        50 back to back: microsecond kernels were hit hardest).  ``ratio`` is the larger."""
-        # the post-init twin streams buffers allocated now, after the communicator exists
-        self.x2 = torch.ones_like(self.x)
-        self.y2 = torch.empty_like(self.x)
-        for _ in range(3):
-            self._run(1)
-        torch.cuda.synchronize()
-        res = {}
-        for name, kw in (("stream", {}), ("small", {"reps": 50, "blocks": 64, "n": 1 << 16})):
-            t0, t1 = [], []
-            for _ in range(rounds):          # interleaved: the same clock state for both
-                t0.append(self._time(0, **kw))
-                t1.append(self._time(1, **kw))
-            t0.sort()
-            t1.sort()
-            a, b = t0[rounds // 2], t1[rounds // 2]
-            res[name] = {"pre_init_us": round(a, 2), "post_init_us": round(b, 2), "ratio": round(b / a, 4)}
-        res["ratio"] = max(res["stream"]["ratio"], res["small"]["ratio"])
-        self.x = self.y = self.x2 = self.y2 = None
-        return res
