@@ -98,7 +98,8 @@ def measure(a) -> dict:
     model = model.to(torch.bfloat16)
     n = sum(p.numel() for p in model.parameters())
     conf = {"optimizer": {"type": "Adam", "params": {"lr": 1e-4}},
-            "zero_optimization": {"stage": a.stage, "reduce_bucket_size": 5e8}}
+            "zero_optimization": {"stage": a.stage, "reduce_bucket_size": 5e8,
+                                  "overlap_optimizer_step": a.overlap_optimizer == "on"}}
     eng, opt, _, _ = initialize(model=model, model_parameters=model.parameters(), config=conf)
     build_s = time.time() - t0
     ds = SyntheticLMDataset(cfg, a.steps + 1, seq_len=a.seq_len, mlm=False, seed=rank)
@@ -125,6 +126,7 @@ def measure(a) -> dict:
            "peak_alloc_GB": round(peak / 1e9, 1), "projected_GB": round(pr.total / 1e9, 1),
            "hbm_GB": round(torch.cuda.get_device_properties(dev).total_memory / 1e9, 1),
            "tokens_per_s": round(world * a.steps * a.seq_len / dt, 1), "build_s": round(build_s, 1),
+           "overlap_optimizer": a.overlap_optimizer,
            "loss_first": round(float(losses[0]), 4), "loss_last": round(float(losses[-1]), 4),
            "finite": bool(all(torch.isfinite(x) for x in losses))}
     comm.destroy()
@@ -140,6 +142,8 @@ def main(argv=None):
     p.add_argument("--hidden", type=int, default=0)
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--seq-len", type=int, default=512)
+    p.add_argument("--overlap-optimizer", default="on", choices=["on", "off"],
+                   help="ZeRO overlap_optimizer_step: each segment's Adam update runs under the rest of the backward")
     a = p.parse_args(argv)
     if not a.measure:
         for r in projection_table(a.fraction):

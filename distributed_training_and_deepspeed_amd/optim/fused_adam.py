@@ -284,6 +284,28 @@ class FusedAdam(torch.optim.Optimizer):
                 ev.record(side)
                 self._events[i] = ev
 
+    # ------------------------------------------------------------------ ranges (overlap with backward)
+    def begin_ranged_step(self) -> None:
+        """Start a step whose update is launched range by range (``step_range``), e.g. by the
+        ZeRO engine as each partition segment's gradient becomes final during the backward: the
+        step counter and hyper-parameters advance once, here, on the current stream.  Needs no
+        global gradient norm (``max_grad_norm`` None)."""
+        assert self.max_grad_norm is None and self.master.is_cuda and self._chunks is None
+        self._push_hparams()
+        self.step_count += 1
+        self.hp[5:6].add_(1.0)
+
+    def step_range(self, a: int, b: int, stream) -> None:
+        """The fused Adam kernel over elements [a, b) of the flat buffers on ``stream`` (per
+        element the same math as the whole-buffer launch: bit-identical results)."""
+        if b <= a:
+            return
+        es, gs, lp = 4, self.grad_flat.element_size(), self.lowp
+        _lib.call("dtd_adam_step", self.master.data_ptr() + a * es, self.exp_avg.data_ptr() + a * es,
+                  self.exp_avg_sq.data_ptr() + a * es, self.grad_flat.data_ptr() + a * gs,
+                  _lib.dt(self.grad_flat), None if lp is None else lp.data_ptr() + a * lp.element_size(),
+                  b - a, self.hp.data_ptr(), self.mode, stream.cuda_stream)
+
     def parameters_ready(self) -> None:
         """Public fence for code that reads parameters outside a stage forward (see the
         contract of overlap_with_forward): the current stream waits for every staged update."""

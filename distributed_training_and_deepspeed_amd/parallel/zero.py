@@ -60,7 +60,8 @@ DEFAULTS = {
     "zero_optimization": {"stage": 0, "reduce_bucket_size": 5e8, "allgather_bucket_size": 5e8,
                           "overlap_comm": None, "stage3_prefetch_bucket_size": 5e7,
                           "overlap_param_refresh": True, "world1_replicated": True,
-                          "force_collectives": False, "stage3_gather_communicator": False},
+                          "force_collectives": False, "stage3_gather_communicator": False,
+                          "overlap_optimizer_step": False},
 }
 
 
@@ -101,6 +102,14 @@ class ZeroConfig:
                                 or os.environ.get("DTD_ZERO_POISON", "0") == "1")
         oc = z.get("overlap_comm")
         self.overlap = (self.stage >= 2) if oc is None else bool(oc)
+        # Adam on each segment's shard as soon as the backward is past it (a side stream), instead
+        # of one launch after the backward.  Opt-in: the update then starts inside backward(), so
+        # the weights change before step() returns -- a loop must pair every backward() with a
+        # step() (the reference scripts do) and not read weights in between.  Needs no gradient
+        # clipping (the global norm is known only after the backward); env DTD_ZERO_OPT_OVERLAP=1/0
+        # overrides the config key.
+        env = os.environ.get("DTD_ZERO_OPT_OVERLAP")
+        self.overlap_opt = bool(z.get("overlap_optimizer_step", False)) if env is None else env == "1"
         bf = cfg.get("bf16", {})
         self.bf16 = bool(bf.get("enabled", False)) if isinstance(bf, dict) else bool(bf)
 
@@ -366,6 +375,11 @@ class ZeroEngine(nn.Module):
         if self.stage == 3:
             self._install_unit_hooks()
         self.optimizer = self._build_optimizer()
+        self.overlap_opt = self.config.overlap_opt
+        self._opt_stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self._opt_started = False    # this step's update began during the backward
+        self._opt_pending = []       # segments reduced, their update not launched yet
+        self._opt_done = set()       # segment indices updated this step
 
     # ================================================================== planning
     def _plan_units(self, model, params):
@@ -720,6 +734,48 @@ class ZeroEngine(nn.Module):
             s.gbuf = None
             for p in s.params:
                 p.main_grad = None
+        self._opt_after_reduce(s)
+
+    # ================================================================== optimizer under the backward
+    def _opt_overlap_active(self) -> bool:
+        return (self.overlap_opt and self.cuda and self.optimizer.max_grad_norm is None
+                and self.optimizer._chunks is None and not self._capturing()
+                and self.is_gradient_accumulation_boundary())
+
+    def _opt_after_reduce(self, s: _Segment) -> None:
+        """Segment ``s`` holds its final gradient shard.  Its Adam update is launched at the NEXT
+        segment's reduce (or in ``step``), not now: the backward call that reported the segment's
+        last gradient may still read its weights (a layer emits its weight gradient before its
+        input-gradient GEMM), and with the world-1 aliases the update writes those weights.  By the
+        next reduce -- the next unit's backward, in reverse layer order -- everything that reads
+        them has been enqueued, so the side stream's update runs beside the rest of the backward."""
+        if not hasattr(self, "_opt_stream") or not self._opt_overlap_active():
+            return
+        if not self._opt_started:
+            self.optimizer.begin_ranged_step()
+            self._opt_started = True
+        self._opt_launch(self._opt_pending)
+        self._opt_pending = [s]
+
+    def _opt_launch(self, segs) -> None:
+        segs = [s for s in segs if s.index not in self._opt_done]
+        if not segs:
+            return
+        side = self._opt_stream
+        side.wait_stream(torch.cuda.current_stream(self.device))   # grads written, weights read
+        if self.comm_stream is not None:
+            side.wait_stream(self.comm_stream)                     # reduce-scatters landed
+        for s in segs:
+            self.optimizer.step_range(s.shard_off, s.shard_off + s.chunk, side)
+            self._opt_done.add(s.index)
+
+    def _opt_finish(self) -> None:
+        """step(): update every segment not yet updated and join the side stream."""
+        self._opt_launch(self.segments)
+        torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
+        self._opt_started = False
+        self._opt_pending = []
+        self._opt_done = set()
 
     def _tmp(self) -> torch.Tensor:
         if self._gtmp is None:
@@ -922,7 +978,10 @@ class ZeroEngine(nn.Module):
         self._join_captured()
         if self._cs() is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
-        self.optimizer.step()
+        if self._opt_started:
+            self._opt_finish()
+        else:
+            self.optimizer.step()
         self._refresh_params()
         self.micro_step = 0
         self.global_steps += 1

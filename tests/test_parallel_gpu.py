@@ -22,19 +22,21 @@ def rccl_world1():
     comm.destroy()
 
 
-def _zero_run(stage, steps=4, replicated=True, force=False):
+def _zero_run(stage, steps=4, replicated=True, force=False, overlap_opt=False):
     from distributed_training_and_deepspeed_amd.parallel.zero import initialize
     model = build_model("causal-tiny", dtype=torch.bfloat16, device="cuda", seed=3)
     cfg = {"optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "comms_logger": {"enabled": True},
            "zero_optimization": {"stage": stage, "reduce_bucket_size": 100000, "world1_replicated": replicated,
-                                 "force_collectives": force}}
+                                 "force_collectives": force, "overlap_optimizer_step": overlap_opt}}
     eng, opt, _, _ = initialize(model=model, model_parameters=model.parameters(), config=cfg)
     ds = SyntheticLMDataset(model.cfg, 4 * steps, seq_len=128, mlm=False, seed=1)
     ids, lab = ds.input_ids.view(steps, 4, 128).cuda(), ds.labels.view(steps, 4, 128).cuda()
     losses = []
+    eng.started_in_backward = []
     for i in range(steps):
         loss = eng(ids[i], labels=lab[i]).loss
         eng.backward(loss)
+        eng.started_in_backward.append(eng._opt_started)
         eng.step()
         losses.append(loss.item())
     torch.cuda.synchronize()
@@ -65,6 +67,29 @@ def test_zero_rccl_collectives_at_world1_match_local_path(rccl_world1, stage):
     assert ef.collect and not el.collect
     assert ll == lf, (ll, lf)
     assert torch.equal(ml, mf)
+
+
+@pytest.mark.parametrize("stage,replicated,force", [(0, True, False), (1, False, False), (2, False, False),
+                                                    (2, False, True), (3, True, False), (3, False, False),
+                                                    (3, False, True)])
+def test_zero_optimizer_overlapped_with_backward_is_bit_identical(rccl_world1, stage, replicated, force):
+    """overlap_optimizer_step: each segment's Adam update launched on a side stream once the
+    backward is past it (stage-3 units one unit late, so a layer's own input-gradient GEMM has read
+    its weights) -- the same kernel per element, so losses and master weights are bit-identical to
+    the single launch in step(), and the update really started inside the backward."""
+    lo, mo, eo = _zero_run(stage, replicated=replicated, force=force)
+    import os as _os
+    os_prev = _os.environ.pop("DTD_ZERO_OPT_OVERLAP", None)
+    try:
+        lv, mv, ev = _zero_run(stage, replicated=replicated, force=force, overlap_opt=True)
+    finally:
+        if os_prev is not None:
+            _os.environ["DTD_ZERO_OPT_OVERLAP"] = os_prev
+    assert ev.overlap_opt and not eo.overlap_opt
+    assert all(ev.started_in_backward) and not any(eo.started_in_backward)
+    assert ev.optimizer.step_count == eo.optimizer.step_count == 4
+    assert lo == lv, (lo, lv)
+    assert torch.equal(mo, mv)
 
 
 def _ddp_run(force, steps=4, overlap=True):
