@@ -142,8 +142,11 @@ def main(argv=None):
     p.add_argument("--hidden", type=int, default=0)
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--seq-len", type=int, default=512)
-    p.add_argument("--overlap-optimizer", default="on", choices=["on", "off"],
-                   help="ZeRO overlap_optimizer_step: each segment's Adam update runs under the rest of the backward")
+    p.add_argument("--overlap-optimizer", default="off", choices=["on", "off"],
+                   help="ZeRO overlap_optimizer_step: each segment's Adam update runs under the rest of the "
+                        "backward.  Off by default: on the 16 B model it measured 3,248 vs 3,283 tokens/s -- the "
+                        "Adam launch's 8 M workgroups hold every CU, so the GEMM beside it waits (3.4 ms "
+                        "instead of 0.3; profiles/r6_mp3_overlap.txt)")
     a = p.parse_args(argv)
     if not a.measure:
         for r in projection_table(a.fraction):
