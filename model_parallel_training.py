@@ -176,13 +176,17 @@ def main():
     print(f"\nTotal Training Time: {elapsed:.2f} seconds")
     print("\nAverage Idle Time per Device:")
     if graphed is not None:
+        # a replayed graph records no per-stage activity marks: the idle time is not measured
         print("(hipGraph replay: the stages' kernels run back to back on one device; no per-stage idle events)")
-    rows = summarize_idle_time(bert, max(n, 1))
+        rows = [["Device", "Avg Idle Time (ms)"]] + [[i, "n/a (graph)"] for i in range(len(bert.group_devices))]
+        print("\n".join(f"{r[0]}\t{r[1]}" for r in rows))
+    else:
+        rows = summarize_idle_time(bert, max(n, 1))
     print(json.dumps({"tokens_per_s": round(n * args.batch_size * args.seq_len / max(elapsed, 1e-9), 1),
                       "timed_steps": n, "graph": graphed is not None,
                       "pipeline": args.pipeline, "stages": len(bert.group_devices),
                       "checkpoint": args.checkpoint if args.pipeline else None,
-                      "idle_ms_per_step": [round(r[1], 3) for r in rows[1:]],
+                      "idle_ms_per_step": [None if isinstance(r[1], str) else round(r[1], 3) for r in rows[1:]],
                       "loss_impl": args.loss,
                       "peak_hbm_gb": [round(torch.cuda.max_memory_allocated(d) / 1e9, 3)
                                       for d in sorted({d for d in bert.group_devices if d.type == "cuda"},
