@@ -814,13 +814,7 @@ __device__ __forceinline__ int colsum_col(int k, int hh) { return (k >> 4) * 32 
 // Query tiles of 64 rows (Q, dO row-major in LDS, double-buffered).
 // DROP / ALIBI are compile-time so that the hot path has no runtime branch (whose register
 // merges cost 16 v_mov per query sub-block) and no bias add without ALiBi.
-// SB (load placement inside a 32-query sub-block): 0 = as the compiler schedules it (it hoists the
-// keep-mask scalar loads and the row-statistics LDS reads between the S / dP MFMAs, and since a
-// scalar load and LDS share lgkmcnt, the next fragment wait becomes lgkmcnt(0): the wave stalls on
-// the masks' L2 round trip mid-chain); 1 = a scheduling barrier after the 8 S / dP MFMAs keeps
-// every such load behind them, so the wait overlaps the MFMAs' drain; 2 = as 1 with the row
-// statistics read at the start of the sub-block, beside the Q / dO fragments.
-template <int D, int OCC, int BM, bool DROP, bool ALIBI, int SB = 0>
+template <int D, int OCC, int BM, bool DROP, bool ALIBI>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   constexpr bool SWZ = D == 64;                 // swizzled unpadded image (swz64_off)
   constexpr int QP = SWZ ? D : D + 8, NC = D / 16, NDB = D / 32;
@@ -921,17 +915,6 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll kQbUnroll
     for (int qb = 0; qb < BM / 32; ++qb) {
       f32x16 sacc = f32x16{}, pacc = f32x16{};
-      // row statistics of this lane's 16 accumulator rows (rows 8g + 4hh + 0..3 are contiguous):
-      // 8 ds_read_b128 issued together instead of 32 dependent scalar LDS reads
-      f32x4 L4[4], D4[4];
-      auto load_rowstats = [&]() {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          L4[g] = *reinterpret_cast<const f32x4*>(&lse_s[buf][qb * 32 + 8 * g + 4 * hh]);
-          D4[g] = *reinterpret_cast<const f32x4*>(&del_s[buf][qb * 32 + 8 * g + 4 * hh]);
-        }
-      };
-      if constexpr (SB == 2) load_rowstats();
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         if constexpr (SWZ) {
@@ -942,7 +925,6 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
           pacc = mfma32(*reinterpret_cast<const bf16x8*>(&O[(qb * 32 + r) * QP + 16 * c + 8 * hh]), vf[c], pacc);
         }
       }
-      if constexpr (SB != 0) __builtin_amdgcn_sched_barrier(0);
       const int qrow0 = q0 + qb * 32;
       // block-uniform predicate (a scalar branch, never a per-element one)
       const bool needmask = (kblk + 128 > S) || (qrow0 + 32 > S) || (a.causal && kblk + 127 > qrow0);
@@ -953,7 +935,14 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) mk[i] = mp[i];
       }
-      if constexpr (SB != 2) load_rowstats();
+      // row statistics of this lane's 16 accumulator rows (rows 8g + 4hh + 0..3 are contiguous):
+      // 8 ds_read_b128 issued together instead of 32 dependent scalar LDS reads
+      f32x4 L4[4], D4[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        L4[g] = *reinterpret_cast<const f32x4*>(&lse_s[buf][qb * 32 + 8 * g + 4 * hh]);
+        D4[g] = *reinterpret_cast<const f32x4*>(&del_s[buf][qb * 32 + 8 * g + 4 * hh]);
+      }
       // P = 2^(s sc2 + kbias - lse): score pairs (i, i+1) share a row group, so the row terms pair up
       const f32x2 sc2v = pk2(sc2, sc2), kb2 = pk2(kbias, kbias);
 #pragma unroll
@@ -1921,25 +1910,9 @@ DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, con
   DTD_LAUNCH_CHECK();
 }
 
-static int dkdv_sb() {
-  const char* e = getenv("DTD_ATTN_DKDV_SB");
-  return e ? atoi(e) : 0;
-}
-
 template <int D, int OCC, int BM>
 static void launch_dkdv(dim3 grid, hipStream_t s, const BwdArgs& a) {
   const bool drop = a.maskB != nullptr, alibi = a.slopes != nullptr;
-  if constexpr (D == 64 && OCC == 2 && BM == 128) {
-    const int sb = dkdv_sb();
-    if (drop && !alibi && sb == 1) {
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, true, false, 1>), grid, dim3(256), 0, s, a);
-      return;
-    }
-    if (drop && !alibi && sb == 2) {
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, true, false, 2>), grid, dim3(256), 0, s, a);
-      return;
-    }
-  }
   if (drop && alibi) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, true, true>), grid, dim3(256), 0, s, a);
   else if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, true, false>), grid, dim3(256), 0, s, a);
   else if (alibi) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, false, true>), grid, dim3(256), 0, s, a);
