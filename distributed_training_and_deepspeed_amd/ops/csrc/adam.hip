@@ -48,12 +48,21 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// One 8-element group per thread (no grid-stride loop) with non-temporal 16-byte loads and
-// stores: every byte is touched exactly once, so keeping it out of L2/MALL only costs reuse
-// that does not exist, and a flat grid keeps more bytes in flight per CU than a 2048-block
-// grid-stride loop (the same change moved the streaming GELU / LayerNorm kernels from ~4.9 to
-// ~6 TB/s, profiles/r1_elementwise_roofline.jsonl).
-template <bool GBF16>
+// One 8-element group per thread (no grid-stride loop) with non-temporal 16-byte stores: every
+// byte is touched exactly once, and a flat grid keeps more bytes in flight per CU than a
+// 2048-block grid-stride loop (the same change moved the streaming GELU / LayerNorm kernels from
+// ~4.9 to ~6 TB/s, profiles/r1_elementwise_roofline.jsonl).  The loads are plain: with four
+// read streams and four write streams per element, cached loads measured 5.24-5.26 TB/s against
+// 5.05-5.09 for non-temporal ones at 1-2 G elements (profiles/r6_adam_forms.jsonl).
+template <bool NT, typename V>
+__device__ __forceinline__ V ld(const V* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+// ILP: independent 8-element groups per thread (all loads issued before any math: more bytes in
+// flight per wave); NTL: non-temporal loads (stores are always non-temporal).
+template <bool GBF16, int ILP = 1, bool NTL = true>
 __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
   const float lr = a.hp[0], b1 = a.hp[1], b2 = a.hp[2], eps = a.hp[3], wd = a.hp[4];
   const float step = a.hp[5], gs = a.hp[6];
@@ -63,48 +72,64 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
     bc2s = sqrtf(1.f - powf(b2, step));
   }
   const size_t ng = a.n / 8;
-  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (i < ng) {
-    f32x4* P = reinterpret_cast<f32x4*>(a.p) + 2 * i;
-    f32x4* M = reinterpret_cast<f32x4*>(a.m) + 2 * i;
-    f32x4* V = reinterpret_cast<f32x4*>(a.v) + 2 * i;
-    f32x4 p0 = __builtin_nontemporal_load(P), p1 = __builtin_nontemporal_load(P + 1);
-    f32x4 m0 = __builtin_nontemporal_load(M), m1 = __builtin_nontemporal_load(M + 1);
-    f32x4 v0 = __builtin_nontemporal_load(V), v1 = __builtin_nontemporal_load(V + 1);
-    float g[8];
-    if constexpr (GBF16) {
-      vload_nt<bf16, 8>((const bf16*)a.g + i * 8, g);
-    } else {
-      const f32x4* G = reinterpret_cast<const f32x4*>(a.g) + 2 * i;
-      const f32x4 g0 = __builtin_nontemporal_load(G), g1 = __builtin_nontemporal_load(G + 1);
+  const size_t base = (size_t)blockIdx.x * blockDim.x * ILP + threadIdx.x;
+  f32x4 p0[ILP], p1[ILP], m0[ILP], m1[ILP], v0[ILP], v1[ILP];
+  float g[ILP][8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { g[j] = g0[j]; g[4 + j] = g1[j]; }
+  for (int u = 0; u < ILP; ++u) {
+    const size_t i = base + (size_t)u * blockDim.x;
+    if (i < ng) {
+      const f32x4* P = reinterpret_cast<const f32x4*>(a.p) + 2 * i;
+      const f32x4* M = reinterpret_cast<const f32x4*>(a.m) + 2 * i;
+      const f32x4* V = reinterpret_cast<const f32x4*>(a.v) + 2 * i;
+      p0[u] = ld<NTL>(P); p1[u] = ld<NTL>(P + 1);
+      m0[u] = ld<NTL>(M); m1[u] = ld<NTL>(M + 1);
+      v0[u] = ld<NTL>(V); v1[u] = ld<NTL>(V + 1);
+      if constexpr (GBF16) {
+        if constexpr (NTL) vload_nt<bf16, 8>((const bf16*)a.g + i * 8, g[u]);
+        else vload<bf16, 8>((const bf16*)a.g + i * 8, g[u]);
+      } else {
+        const f32x4* G = reinterpret_cast<const f32x4*>(a.g) + 2 * i;
+        const f32x4 g0 = ld<NTL>(G), g1 = ld<NTL>(G + 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { g[u][j] = g0[j]; g[u][4 + j] = g1[j]; }
+      }
     }
-    float q[8], mm[8], vv[8];
+  }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      q[j] = p0[j]; q[4 + j] = p1[j];
-      mm[j] = m0[j]; mm[4 + j] = m1[j];
-      vv[j] = v0[j]; vv[4 + j] = v1[j];
+  for (int u = 0; u < ILP; ++u) {
+    const size_t i = base + (size_t)u * blockDim.x;
+    if (i < ng) {
+      float q[8], mm[8], vv[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        q[j] = p0[u][j]; q[4 + j] = p1[u][j];
+        mm[j] = m0[u][j]; mm[4 + j] = m1[u][j];
+        vv[j] = v0[u][j]; vv[4 + j] = v1[u][j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) adam_elem(q[j], mm[j], vv[j], g[u][j] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
+      f32x4 o0, o1, n0, n1, w0, w1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o0[j] = q[j]; o1[j] = q[4 + j];
+        n0[j] = mm[j]; n1[j] = mm[4 + j];
+        w0[j] = vv[j]; w1[j] = vv[4 + j];
+      }
+      f32x4* P = reinterpret_cast<f32x4*>(a.p) + 2 * i;
+      f32x4* M = reinterpret_cast<f32x4*>(a.m) + 2 * i;
+      f32x4* V = reinterpret_cast<f32x4*>(a.v) + 2 * i;
+      __builtin_nontemporal_store(o0, P); __builtin_nontemporal_store(o1, P + 1);
+      __builtin_nontemporal_store(n0, M); __builtin_nontemporal_store(n1, M + 1);
+      __builtin_nontemporal_store(w0, V); __builtin_nontemporal_store(w1, V + 1);
+      if (a.p_lp) vstore_nt<bf16, 8>(a.p_lp + i * 8, q);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) adam_elem(q[j], mm[j], vv[j], g[j] * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      p0[j] = q[j]; p1[j] = q[4 + j];
-      m0[j] = mm[j]; m1[j] = mm[4 + j];
-      v0[j] = vv[j]; v1[j] = vv[4 + j];
-    }
-    __builtin_nontemporal_store(p0, P); __builtin_nontemporal_store(p1, P + 1);
-    __builtin_nontemporal_store(m0, M); __builtin_nontemporal_store(m1, M + 1);
-    __builtin_nontemporal_store(v0, V); __builtin_nontemporal_store(v1, V + 1);
-    if (a.p_lp) vstore_nt<bf16, 8>(a.p_lp + i * 8, q);
   }
   // tail (n % 8 elements): the first threads of the last block
   const size_t e = ng * 8 + threadIdx.x;
   if (blockIdx.x == gridDim.x - 1 && e < a.n) {
-    float g = GBF16 ? (float)((const bf16*)a.g)[e] : ((const float*)a.g)[e];
-    adam_elem(a.p[e], a.m[e], a.v[e], g * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
+    float gt = GBF16 ? (float)((const bf16*)a.g)[e] : ((const float*)a.g)[e];
+    adam_elem(a.p[e], a.m[e], a.v[e], gt * gs, lr, b1, b2, eps, wd, bc1, bc2s, a.mode);
     if (a.p_lp) a.p_lp[e] = (bf16)a.p[e];
   }
 }
@@ -156,10 +181,25 @@ DTD_EXPORT int dtd_adam_step(float* p, float* m, float* v, const void* g, int g_
                              const float* hp, int mode, hipStream_t s) {
   if (n == 0) return 0;
   AdamArgs a{p, m, v, g, (bf16*)p_lp, n, hp, mode, g_dtype};
-  // 8 elements per thread; at least one block so the tail always has an owner
-  const size_t blocks = (n / 8 + 255) / 256 > 0 ? (n / 8 + 255) / 256 : 1;
-  if (g_dtype == kBF16) hipLaunchKernelGGL(adam_kernel<true>, dim3(blocks), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(adam_kernel<false>, dim3(blocks), dim3(256), 0, s, a);
+  // DTD_ADAM_FORM (measurement knob): 1c (default) = one 8-element group per thread, cached
+  // loads; 2c = two groups per thread; 1 / 2 = the same with non-temporal loads
+  const char* fe = getenv("DTD_ADAM_FORM");
+  const int form = fe ? (fe[0] == '2' ? 2 : 1) + (fe[0] && fe[1] == 'c' ? 10 : 0) : 11;
+  const int ilp = form % 10;
+  // 8 elements per thread and group; at least one block so the tail always has an owner
+  const size_t per = 256 * (size_t)ilp;
+  const size_t blocks = (n / 8 + per - 1) / per > 0 ? (n / 8 + per - 1) / per : 1;
+  const bool bf = g_dtype == kBF16;
+  switch (form) {
+    case 2: if (bf) hipLaunchKernelGGL((adam_kernel<true, 2, true>), dim3(blocks), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((adam_kernel<false, 2, true>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 11: if (bf) hipLaunchKernelGGL((adam_kernel<true, 1, false>), dim3(blocks), dim3(256), 0, s, a);
+             else hipLaunchKernelGGL((adam_kernel<false, 1, false>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 12: if (bf) hipLaunchKernelGGL((adam_kernel<true, 2, false>), dim3(blocks), dim3(256), 0, s, a);
+             else hipLaunchKernelGGL((adam_kernel<false, 2, false>), dim3(blocks), dim3(256), 0, s, a); break;
+    default: if (bf) hipLaunchKernelGGL((adam_kernel<true, 1, true>), dim3(blocks), dim3(256), 0, s, a);
+             else hipLaunchKernelGGL((adam_kernel<false, 1, true>), dim3(blocks), dim3(256), 0, s, a); break;
+  }
   DTD_LAUNCH_CHECK();
 }
 
