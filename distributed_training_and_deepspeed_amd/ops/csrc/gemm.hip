@@ -90,7 +90,14 @@ struct GemmArgs {
   unsigned long long* stamps;            // diagnostic builds only (-DDTD_GEMM_STAMPS), else null
   int* sched;                            // persistent form: dynamic tile queue (see below) or null
   int stagger;                           // persistent form: start delay (10 ns ticks) of odd members
+  int nt;                                // persistent form: non-temporal epilogue stores (DTD_GEMM_NT_STORE)
 };
+
+// 16-byte epilogue store, non-temporal when `nt` (a wave-uniform flag)
+__device__ __forceinline__ void st8(bf16* p, const bf16x8& v, int nt) {
+  if (nt) __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
+  else *reinterpret_cast<bf16x8*>(p) = v;
+}
 
 // Dynamic tile queue of the persistent form: sched[x] (x = 0..7) is the next unclaimed tile of XCD
 // group x (after the 2 x 32 tiles per group the static order hands out first), sched[8] counts finished
@@ -781,18 +788,18 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + r * 512 + ((c ^ (r & 15)) << 4));
         const size_t off = (size_t)(m0 + rr * 128 + r) * g.ldc + n0 + c * 8;
         if constexpr (EPI == EPI_STORE || EPI == EPI_ADD) {
-          *reinterpret_cast<bf16x8*>(g.c + off) = v;
+          st8(g.c + off, v, g.nt);
         } else if constexpr (stores_grad(EPI)) {
           float av[8], dv[8];
           act_and_grad8<EPI>(v, av, dv);
-          *reinterpret_cast<bf16x8*>(g.c + off) = cvt8(dv);
-          *reinterpret_cast<bf16x8*>(g.c2 + off) = cvt8(av);
+          st8(g.c + off, cvt8(dv), g.nt);
+          st8(g.c2 + off, cvt8(av), g.nt);
         } else if constexpr (is_gelu_fwd(EPI)) {
           bf16x8 av;
 #pragma unroll
           for (int j = 0; j < 8; ++j) av[j] = (bf16)epi_act<EPI>((float)v[j]);
-          *reinterpret_cast<bf16x8*>(g.c + off) = v;
-          *reinterpret_cast<bf16x8*>(g.c2 + off) = av;
+          st8(g.c + off, v, g.nt);
+          st8(g.c2 + off, av, g.nt);
         } else {
           float o[8];
 #pragma unroll
@@ -800,7 +807,7 @@ __global__ void __launch_bounds__(512, 2) gemm_bt_persistent(GemmArgs g) {
             o[j] = (float)v[j] * epi_act_grad<EPI>((float)uin[rr][i][j]);
             colsum[j] += o[j];
           }
-          *reinterpret_cast<bf16x8*>(g.c + off) = cvt8(o);
+          st8(g.c + off, cvt8(o), g.nt);
         }
       }
       if (dyn && rr == 1 && tid == 0) qslot[(it + 1) & 1] = has_next ? beg + 2 * per + claim : end;
@@ -940,6 +947,14 @@ static int num_cus() {
   return n;
 }
 
+// persistent-form non-temporal epilogue stores (default; DTD_GEMM_NT_STORE=0 turns them off, read
+// per call): the fused FFN kernels write two T x 3072 tensors per layer that nothing reads from
+// cache -- +0.13 % step at b1024, the same in both interleaved rounds (profiles/r6_ntstore.jsonl)
+static int gemm_nt_store() {
+  const char* e = getenv("DTD_GEMM_NT_STORE");
+  return !(e && e[0] == '0');
+}
+
 // persistent-form start stagger in 10 ns ticks (DTD_GEMM_STAGGER_US; dtd_gemm_set_stagger)
 static int g_stagger = -1;
 static int gemm_stagger() {
@@ -982,7 +997,7 @@ DTD_EXPORT int dtd_gemm_bt(int epi, const void* a, int lda, const void* b, int l
   if (is_gelu_fwd(epi) && !c2) return (int)hipErrorInvalidValue;
   if (is_gelu_bwd(epi) && !u) return (int)hipErrorInvalidValue;
   GemmArgs g{(const bf16*)a, (const bf16*)b, (bf16*)c, (bf16*)c2, (const bf16*)u, (const bf16*)bias, part,
-             M, N, K, lda, ldb, ldc, ldu, g_stamps, nullptr, gemm_stagger()};
+             M, N, K, lda, ldb, ldc, ldu, g_stamps, nullptr, gemm_stagger(), gemm_nt_store()};
   const int ntiles = (M / BM) * (N / BN);
   if (gemm_variant() >= 1) {
     const int cus = num_cus() / 8 * 8;
