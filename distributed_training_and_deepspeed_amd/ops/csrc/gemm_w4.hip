@@ -76,7 +76,8 @@ struct Sched {
   static_assert(DMA0 > 19 && dma_slot(15) < 128 && nb2 < 16 && B2I + 31 < 64, "K-step schedule");
 };
 // (the round-6 sweep over DMA0 20-21, DSTEP 6-7, B2I 16-30 measured all forms within 1 %,
-// profiles/r6_w4_sched.jsonl; two are kept)
+// profiles/r6_w4_sched.jsonl; two are kept.  Non-temporal epilogue stores lost 1 %: the next kernel
+// reads these outputs, profiles/r6_w4nt.jsonl)
 #define DTD_W4_SCHEDS(X) X(0, 20, 7, 24) X(1, 20, 6, 24)
 constexpr int SCHED_COUNT = 2, SCHED_DEFAULT = 0;
 
@@ -409,7 +410,12 @@ int num_cus() {
 
 }  // namespace
 
-static int g_sched = SCHED_DEFAULT;
+// DTD_GEMM_W4_SCHED: the schedule variant at load (A/B runs); dtd_gemm_w4_set_sched at run time
+static int g_sched = [] {
+  const char* e = getenv("DTD_GEMM_W4_SCHED");
+  const int i = e ? atoi(e) : SCHED_DEFAULT;
+  return i >= 0 && i < SCHED_COUNT ? i : SCHED_DEFAULT;
+}();
 DTD_EXPORT int dtd_gemm_w4_set_sched(int i) {
   if (i < 0 || i >= SCHED_COUNT) return (int)hipErrorInvalidValue;
   g_sched = i;
