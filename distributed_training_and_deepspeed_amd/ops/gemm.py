@@ -201,6 +201,10 @@ def gemm_f32_tn(a: torch.Tensor, b: torch.Tensor, splits: int | None = None) -> 
 _W4 = [os.environ.get("DTD_GEMM_W4", "1") == "1"]
 _W4_ADD = [os.environ.get("DTD_GEMM_W4_ADD", "0") == "1"]
 _W4_MIN_TILES = [int(os.environ.get("DTD_GEMM_W4_MIN_TILES", "0")) or None]
+# Long-K products (K = 3072: the fc2 forward and the fc1 input gradient) run 0.95-0.96x the library
+# on it on every box measured (profiles/r6_w4_sched.jsonl, profiles/r6_w4nt.jsonl) while the
+# K <= 2304 ones run 1.0-1.18x: the dispatch keeps K above DTD_GEMM_W4_MAX_K on hipBLASLt.
+_W4_MAX_K = [int(os.environ.get("DTD_GEMM_W4_MAX_K", "2304"))]
 
 
 def w4_enabled() -> bool:
@@ -242,7 +246,8 @@ def hand_kernels_at_any_size(library: bool = True):
 
 def _w4_pick(M: int, N: int, K: int, *tensors) -> bool:
     """The dispatch rule: kernel on, shape tiles, and enough tiles to fill the persistent grid."""
-    return (w4_enabled() and (M // 256) * (N // 256) >= w4_min_tiles() and w4_supported(M, N, K, *tensors))
+    return (w4_enabled() and K <= _W4_MAX_K[0] and (M // 256) * (N // 256) >= w4_min_tiles()
+            and w4_supported(M, N, K, *tensors))
 
 
 def gemm_w4(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None,
