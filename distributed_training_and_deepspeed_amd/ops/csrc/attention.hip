@@ -814,7 +814,11 @@ __device__ __forceinline__ int colsum_col(int k, int hh) { return (k >> 4) * 32 
 // Query tiles of 64 rows (Q, dO row-major in LDS, double-buffered).
 // DROP / ALIBI are compile-time so that the hot path has no runtime branch (whose register
 // merges cost 16 v_mov per query sub-block) and no bias add without ALiBi.
-template <int D, int OCC, int BM, bool DROP, bool ALIBI>
+// MASK = false: the launch knows no block needs the causal / sequence-end mask (not causal, S a
+// multiple of 128).  The runtime `needmask` branch alone is not enough: hipcc hoists the 16 key /
+// query comparisons and their lane-mask combines above it, 48 VALU + 52 SALU per 32-query
+// sub-block executed on every interior block.
+template <int D, int OCC, int BM, bool DROP, bool ALIBI, bool MASK = true>
 __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
   constexpr bool SWZ = D == 64;                 // swizzled unpadded image (swz64_off)
   constexpr int QP = SWZ ? D : D + 8, NC = D / 16, NDB = D / 32;
@@ -927,7 +931,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
       }
       const int qrow0 = q0 + qb * 32;
       // block-uniform predicate (a scalar branch, never a per-element one)
-      const bool needmask = (kblk + 128 > S) || (qrow0 + 32 > S) || (a.causal && kblk + 127 > qrow0);
+      const bool needmask = MASK && ((kblk + 128 > S) || (qrow0 + 32 > S) || (a.causal && kblk + 127 > qrow0));
       // this query block's keep masks (after the S / dP MFMAs consumed their LDS operands)
       uint64_t mk[16];
       if constexpr (DROP) {
@@ -953,7 +957,7 @@ __global__ void __launch_bounds__(256, OCC) attn_bwd_dkdv_kernel(BwdArgs a) {
         sacc[i] = fexp2(x.x);
         sacc[i + 1] = fexp2(x.y);
       }
-      if (needmask) {
+      if (MASK && needmask) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int qq = qrow0 + crow(i, hh);
@@ -1913,6 +1917,11 @@ DTD_EXPORT int dtd_attn_masks(uint32_t* masks, int B, int S, int H, float p, con
 template <int D, int OCC, int BM>
 static void launch_dkdv(dim3 grid, hipStream_t s, const BwdArgs& a) {
   const bool drop = a.maskB != nullptr, alibi = a.slopes != nullptr;
+  if (!a.causal && a.S % 128 == 0 && !alibi) {   // no block needs the mask (BERT: S = 512)
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, true, false, false>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, false, false, false>), grid, dim3(256), 0, s, a);
+    return;
+  }
   if (drop && alibi) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, true, true>), grid, dim3(256), 0, s, a);
   else if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, true, false>), grid, dim3(256), 0, s, a);
   else if (alibi) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, OCC, BM, false, true>), grid, dim3(256), 0, s, a);
