@@ -113,7 +113,10 @@ template <int N> __device__ __forceinline__ void wait_vm() { asm volatile("s_wai
 // younger K-steps in flight.
 // DIAG (timing-only builds, wrong results unless 0): 1 = no LDS-DMA in the K loop (stale stages),
 // 2 = no barrier in the K loop, 4 = no fragment reads in the K loop (stale registers)
-template <int NBUF, bool UNROLL, int DIAG = 0>
+// SPREAD: the K-step's 4 DMA pieces go out with MFMA groups 0, 2, 4, 6 instead of 0-3 (one per 8
+// MFMAs instead of one per 4 in the first half; the pieces' issue cost queued at the texture unit
+// when bunched in gemm_w4.hip, profiles/r6_w4_pmc_bunched_dma.json)
+template <int NBUF, bool UNROLL, int DIAG = 0, bool SPREAD = false>
 __global__ void __launch_bounds__(512, 2) wgrad_tn_kernel(WgArgs g) {
   static_assert(NBUF >= 4 && NBUF <= 5 && (!UNROLL || NBUF == 4), "ring depth");
   constexpr int DMA = 4;                    // LDS-DMA instructions per wave per K-step
@@ -227,7 +230,11 @@ __global__ void __launch_bounds__(512, 2) wgrad_tn_kernel(WgArgs g) {
         asm volatile("" : "+v"(a[(mi + 2) & 3]));
         if (mi & 1) asm volatile("" : "+v"(bn[mi >> 1]));
       }
-      if (!(DIAG & 1) && mi < DMA) dma(prv, issue_k, mi);
+      if constexpr (SPREAD) {
+        if (!(DIAG & 1) && (mi & 1) == 0) dma(prv, issue_k, mi >> 1);
+      } else {
+        if (!(DIAG & 1) && mi < DMA) dma(prv, issue_k, mi);
+      }
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(bc[ni], a[mi & 3], acc[mi][ni]);
       // keep each group's reads in their group: left alone the scheduler sinks a read down to the
@@ -319,11 +326,17 @@ DTD_EXPORT int dtd_wgrad_tn(int variant, const void* a, int lda, const void* b, 
   if (rows * lda * 2 >= 0x7fffffffull || rows * ldb * 2 >= 0x7fffffffull) return (int)hipErrorInvalidValue;
   WgArgs g{(const bf16*)a, (const bf16*)b, (float*)part, M, N, K, lda, ldb, splits, ksplit};
   const int nwg = (M / BM) * (N / BN) * splits;
-  if (variant == 0) variant = 44;   // 128 KiB: leaves LDS for a co-resident side-stream kernel
+  if (variant == 0) {   // 46: 128 KiB (leaves LDS for a co-resident side-stream kernel), spread DMA:
+    // 5697 vs 5736 us per b1024 layer, +0.2 % step in both interleaved rounds
+    // (profiles/r6_wgrad_spread.jsonl); DTD_WGRAD_VARIANT=44 restores the bunched pieces
+    const char* e = getenv("DTD_WGRAD_VARIANT");
+    variant = e ? atoi(e) : 46;
+  }
   switch (variant) {
     case 4: hipLaunchKernelGGL((wgrad_tn_kernel<4, false>), dim3(nwg), dim3(512), 0, s, g); break;
     case 5: hipLaunchKernelGGL((wgrad_tn_kernel<5, false>), dim3(nwg), dim3(512), 0, s, g); break;
     case 44: hipLaunchKernelGGL((wgrad_tn_kernel<4, true>), dim3(nwg), dim3(512), 0, s, g); break;
+    case 46: hipLaunchKernelGGL((wgrad_tn_kernel<4, true, 0, true>), dim3(nwg), dim3(512), 0, s, g); break;
     // diagnostic (timing-only) builds of variant 44: 440 + DIAG
     case 441: hipLaunchKernelGGL((wgrad_tn_kernel<4, true, 1>), dim3(nwg), dim3(512), 0, s, g); break;
     case 442: hipLaunchKernelGGL((wgrad_tn_kernel<4, true, 2>), dim3(nwg), dim3(512), 0, s, g); break;
