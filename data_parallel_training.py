@@ -50,6 +50,9 @@ from distributed_training_and_deepspeed_amd.utils.tracing import StepTimer, enab
 
 def train(rank, world_size, batch_size, training_steps, bucket_size, model_name, opts):
     backend = opts.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        from distributed_training_and_deepspeed_amd.utils.tuning import maybe_use_tuned_gemms
+        maybe_use_tuned_gemms()   # measured hipBLASLt solutions (incl. this script's default shapes)
     if backend == "nccl" and prewarm_enabled():
         # the step's kernels run once before the RCCL communicator exists: kernels first launched
         # after it run 5-25 % slower for the life of the process (utils/prewarm.py)

@@ -90,6 +90,9 @@ def main():
                         help="stage-per-process mode (launched with several ranks): the point-to-point "
                              "transport; auto = RCCL on GPUs, gloo on CPU")
     args = parser.parse_args()
+    if torch.cuda.is_available():
+        from distributed_training_and_deepspeed_amd.utils.tuning import maybe_use_tuned_gemms
+        maybe_use_tuned_gemms()   # measured hipBLASLt solutions
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         return main_stage_per_process(args)
 
