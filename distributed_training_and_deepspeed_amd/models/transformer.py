@@ -280,9 +280,10 @@ def _acc(p):
 def _ffn_gemm_ok(c, x: torch.Tensor, w: torch.Tensor, *more) -> bool:
     """The hand-written GEMM with the GELU epilogues (ops/csrc/gemm.hip) takes the FFN products
     when the activation is GELU (erf or tanh), the tensors are bf16 on the GPU and the shape tiles
-    by 256."""
+    by 256 into at least a tile per CU (``G.ffn_tiles_ok``)."""
     return (c.activation in G.FUSED_ACTS and x.is_cuda and x.dtype == torch.bfloat16 and G.enabled()
-            and G.supported(x.shape[0], w.shape[0], x.shape[1], x, w, *more))
+            and G.supported(x.shape[0], w.shape[0], x.shape[1], x, w, *more)
+            and G.ffn_tiles_ok(x.shape[0], w.shape[0]))
 
 
 def _proj_ln(inp, w, bias, res, gamma, beta, eps, p, rng, sid, store_z):
@@ -390,7 +391,8 @@ class _FusedLayerFn(torch.autograd.Function):
         # recomputed inside the activation-backward pass (no separate act_fwd read/write)
         w2t = None
         if (a is not None and G.ffn_bwd_enabled() and c.activation in G.FUSED_ACTS and dy.is_cuda
-                and dy.dtype == torch.bfloat16 and G.supported(dy.shape[0], w2.shape[1], dy.shape[1], dy, u)):
+                and dy.dtype == torch.bfloat16 and G.supported(dy.shape[0], w2.shape[1], dy.shape[1], dy, u)
+                and G.ffn_tiles_ok(dy.shape[0], w2.shape[1])):
             w2t = G.transposed(w2)                     # [ffn, hidden]: K-contiguous B operand
         if ctx.ffn_g:
             # u holds act'(u): dU = dA * u

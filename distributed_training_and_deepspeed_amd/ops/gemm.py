@@ -82,6 +82,18 @@ def enabled() -> bool:
     return _ENABLED[0]
 
 
+# The fused FFN kernels run one 256 x 256 tile per workgroup: below about one tile per CU (batch 1-4
+# at seq 512: 32-96 tiles) most of the chip idles, and hipBLASLt's small-tile kernels plus the
+# separate activation pass are faster (DTD_GEMM_FFN_MIN_TILES; default: the CU count).
+_FFN_MIN_TILES = [int(os.environ.get("DTD_GEMM_FFN_MIN_TILES", "0")) or None]
+
+
+def ffn_tiles_ok(M: int, N: int) -> bool:
+    if _FFN_MIN_TILES[0] is None:
+        _FFN_MIN_TILES[0] = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return (M // 256) * (N // 256) >= _FFN_MIN_TILES[0]
+
+
 def ffn_fwd_enabled() -> bool:
     return _ENABLED[0] and _FFN_FWD[0]
 
@@ -231,17 +243,19 @@ def w4_min_tiles() -> int:
 
 @contextlib.contextmanager
 def hand_kernels_at_any_size(library: bool = True):
-    """Within the block the one-wave-per-SIMD kernel takes every product it tiles, whatever its
-    tile count (and with ``library=False`` the 8-wave kernel the rest it tiles): the prewarm's
-    batch-1 step (utils/prewarm.py) then launches the kernels the real step will use."""
-    prev = (_W4_MIN_TILES[0], _ALL[0])
+    """Within the block the one-wave-per-SIMD kernel and the fused FFN kernels take every product
+    they tile, whatever its tile count (and with ``library=False`` the 8-wave kernel the rest it
+    tiles): the prewarm's batch-1 step (utils/prewarm.py) then launches the kernels the real step
+    will use."""
+    prev = (_W4_MIN_TILES[0], _FFN_MIN_TILES[0], _ALL[0])
     _W4_MIN_TILES[0] = 1
+    _FFN_MIN_TILES[0] = 1
     if not library:
         _ALL[0] = True
     try:
         yield
     finally:
-        _W4_MIN_TILES[0], _ALL[0] = prev
+        _W4_MIN_TILES[0], _FFN_MIN_TILES[0], _ALL[0] = prev
 
 
 def _w4_pick(M: int, N: int, K: int, *tensors) -> bool:
