@@ -27,9 +27,22 @@ CASES = [
 ]
 
 
+@pytest.fixture(params=[False, True], ids=["ffn_by_tiles", "ffn_fused_always"])
+def ffn_fused(request):
+    """The fused FFN GEMMs (fc1 + GELU, fc2 input gradient + GELU') take a product only from one
+    tile per CU (ops/gemm.py ffn_tiles_ok), so these small models run the unfused path by default;
+    the second parametrisation lifts the rule and runs the fused kernels in the same model."""
+    from distributed_training_and_deepspeed_amd.ops import gemm as G
+    prev = G._FFN_MIN_TILES[0]
+    if request.param:
+        G._FFN_MIN_TILES[0] = 1
+    yield request.param
+    G._FFN_MIN_TILES[0] = prev
+
+
 @pytest.mark.parametrize("name,extra", CASES)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_fused_gpu_matches_reference(name, extra, dtype):
+def test_fused_gpu_matches_reference(name, extra, dtype, ffn_fused):
     cfg, ref, fus = _pair(name, extra, dtype)
     ds = SyntheticLMDataset(cfg, 4, seq_len=128, seed=5)
     ids, lab = ds.input_ids, ds.labels
