@@ -40,6 +40,7 @@ _SIGS = {
     "dtd_act_bwd": (I, [I, P, P, P, P, P, I, I, I, P]),
     "dtd_colsum_finalize": (I, [P, I, I, P, I, I, F, P]),
     "dtd_colsum_finalize_multi": (I, [I, P, I, I, P, I, I, P, I, I, P, I, I, P]),
+    "dtd_colsum_finalize_batch": (I, [I, P, P]),
     "dtd_embed_word_bwd_chunked": (I, [I, I, P, P, P, P, P, P, P, I, I, I, I, P]),
     # xent.hip
     "dtd_xent_fwd": (I, [I, P, P, P, P, P, I, I, I, P]),

@@ -8,6 +8,9 @@ which is how the framework avoids a separate gradient-accumulation pass.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import torch
 
 from . import _lib
@@ -126,12 +129,80 @@ def _finalize_stream(part: torch.Tensor, defer: bool = True) -> int:
     return side.cuda_stream
 
 
+# Batched finalizes.  Inside an autograd backward the column-sum finalizes (bias / LayerNorm
+# gradients from fp32 partials) are queued and launched together -- one kernel per batch of up to 32
+# (``dtd_colsum_finalize_batch``) -- when something is about to read a gradient: the DDP / ZeRO
+# reducers flush before they launch a bucket's collective, and the end of the backward flushes the
+# rest (an autograd-engine callback).  The queue holds the partial buffers, so the caching
+# allocator cannot hand their memory to a later kernel first.  DTD_FINALIZE_BATCH=0: launch each
+# finalize where it is issued (the round-5 behaviour).
+_BATCH = [os.environ.get("DTD_FINALIZE_BATCH", "1") == "1"]
+_PENDING: list = []        # (stream handle, job tuple, keep-alive tensors)
+_PENDING_DST: set = set()
+_CB_QUEUED = [False]
+
+
+class _Job(ctypes.Structure):
+    _fields_ = [("part", ctypes.c_void_p), ("out", ctypes.c_void_p), ("nparts", ctypes.c_int), ("cols", ctypes.c_int),
+                ("dtype", ctypes.c_int), ("acc", ctypes.c_int), ("scale", ctypes.c_float), ("pad", ctypes.c_int)]
+
+
+def set_finalize_batching(on: bool) -> None:
+    flush_finalizes()
+    _BATCH[0] = bool(on)
+
+
+def _batching(part: torch.Tensor) -> bool:
+    return (_BATCH[0] and part.is_cuda and _lib.has("dtd_colsum_finalize_batch")
+            and torch._C._current_graph_task_id() != -1)
+
+
+def _queue(stream: int, jobs, keep) -> None:
+    """Queue finalize jobs (part_ptr, out_ptr, nparts, cols, dtype, acc, scale) on ``stream``."""
+    dsts = {j[1] for j in jobs}
+    if dsts & _PENDING_DST:      # a second finalize into the same gradient: keep them ordered
+        flush_finalizes()
+    for j in jobs:
+        _PENDING.append((stream, j, keep))
+        _PENDING_DST.add(j[1])
+    if not _CB_QUEUED[0]:
+        _CB_QUEUED[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+
+
+def _end_of_backward() -> None:
+    _CB_QUEUED[0] = False
+    flush_finalizes()
+
+
+def flush_finalizes() -> None:
+    """Launch every queued finalize (on the stream it was issued on, in issue order)."""
+    if not _PENDING:
+        return
+    pending = list(_PENDING)
+    _PENDING.clear()
+    _PENDING_DST.clear()
+    i = 0
+    while i < len(pending):
+        stream = pending[i][0]
+        batch = []
+        while i < len(pending) and pending[i][0] == stream and len(batch) < 32:
+            batch.append(pending[i][1])
+            i += 1
+        arr = (_Job * len(batch))(*[_Job(*j, 0) for j in batch])
+        _lib.call("dtd_colsum_finalize_batch", len(batch), ctypes.addressof(arr), stream)
+
+
 def _finalize(part: torch.Tensor, n: int, cols: int, dst, acc: bool, scale: float = 1.0, defer: bool = True):
     if dst is None:
         return
     dst, acc = _unpack(dst, acc)
+    stream = _finalize_stream(part, defer)
+    if stream == _lib.stream() and _batching(part):
+        _queue(stream, [(part.data_ptr(), dst.data_ptr(), n, cols, _lib.dt(dst), int(acc), float(scale))], (part, dst))
+        return
     _lib.call("dtd_colsum_finalize", part.data_ptr(), n, cols, dst.data_ptr(), _lib.dt(dst), int(acc),
-              float(scale), _finalize_stream(part, defer))
+              float(scale), stream)
 
 
 def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: int,
@@ -205,7 +276,15 @@ def ln_bwd(dout, dz_extra, z, mean, rstd, gamma, p: float, rng: RngState, sid: i
             else:
                 t, a = _unpack(d, acc)
                 args += [t.data_ptr(), _lib.dt(t), int(a)]
-        _lib.call("dtd_colsum_finalize_multi", len(dsts), part.data_ptr(), n, h, *args, _finalize_stream(part))
+        stream = _finalize_stream(part)
+        if stream == _lib.stream() and _batching(part):
+            jobs = []
+            for i, d in enumerate(dsts):
+                t, a = _unpack(d, acc)
+                jobs.append((part.data_ptr() + i * n * h * 4, t.data_ptr(), n, h, _lib.dt(t), int(a), 1.0))
+            _queue(stream, jobs, (part, [_unpack(d, acc)[0] for d in dsts]))
+        else:
+            _lib.call("dtd_colsum_finalize_multi", len(dsts), part.data_ptr(), n, h, *args, stream)
     return dz, dy
 
 

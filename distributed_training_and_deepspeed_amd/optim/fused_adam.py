@@ -171,6 +171,7 @@ class FusedAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        Fx.flush_finalizes()  # a backward's batched bias / LayerNorm finalizes (normally flushed at its end)
         self.synchronize()   # staged updates of the previous step: hp / gradients are rewritten below
         if self.gbuf is not None:  # gradients assigned to p.grad by hand (not via autograd)
             for p in self._params:

@@ -42,6 +42,7 @@ import torch.distributed as dist
 from torch import nn
 
 from ..comm import logger as comm_log
+from ..ops.functional import flush_finalizes
 from ..ops.grad import join_async_wgrad, set_async_wgrad, set_defer_finalize
 from ..ops.grad import _ASYNC as _ASYNC_WGRAD
 from ..runtime import ReadyTracker, assign_buckets
@@ -242,6 +243,7 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, b: _Bucket) -> None:
         if not self.collectives:
             return
+        flush_finalizes()   # queued bias / LayerNorm finalizes write into this bucket
         view = self.grads.buf[b.start:b.end]
         if self._xgmi is not None and self._xgmi.supports(view):
             join_async_wgrad(self.device)
@@ -268,6 +270,7 @@ class DistributedDataParallel(nn.Module):
         if not self._sync_enabled:
             # a no_sync micro-step: its side-stream finalizes wrote main_grad; join them before
             # anything else (logging, the next micro-step's autograd-path adds) touches it
+            flush_finalizes()
             join_async_wgrad(self.device)
             set_defer_finalize(False)
             return
@@ -276,6 +279,7 @@ class DistributedDataParallel(nn.Module):
     def finish(self) -> None:
         """Launch any bucket not yet launched (unused parameters get zero gradients) and make
         the current stream wait for every all-reduce."""
+        flush_finalizes()               # batched finalizes still queued by this backward
         join_async_wgrad(self.device)   # async wgrad GEMMs / deferred finalizes
         set_defer_finalize(False)
         self.grads.zero_untouched_()

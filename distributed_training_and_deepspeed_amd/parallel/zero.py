@@ -47,6 +47,7 @@ from torch import nn
 
 from .. import comm
 from ..comm import logger as clog
+from ..ops.functional import flush_finalizes
 from ..optim.fused_adam import FusedAdam
 from ..runtime import ReadyTracker
 from .flat import ALIGN, unique_params
@@ -677,6 +678,7 @@ class ZeroEngine(nn.Module):
     def _reduce_segment(self, s: _Segment) -> None:
         """Reduce one segment's gradients: all-reduce (stage 0) or reduce-scatter into the
         local gradient shard (stages 1-3); stage 2/3 landing regions go back to the arena."""
+        flush_finalizes()   # queued bias / LayerNorm finalizes may write into this segment
         s.launched = True
         if s.gbuf is None:   # no parameter of this segment got a gradient yet: land it now
             self._alloc_landing(s)
@@ -784,6 +786,7 @@ class ZeroEngine(nn.Module):
 
     def _end_of_backward(self) -> None:
         self._callback_queued = False
+        flush_finalizes()
         if (self.stage <= 1 or self.replicated) and not self.is_gradient_accumulation_boundary():
             return
         for s in self.buckets:

@@ -252,3 +252,29 @@ def test_all_native_gemm_mode_matches_library_gemms(monkeypatch):
     assert abs(out[0][0] - out[1][0]) <= 1e-2 * abs(out[0][0])
     g0, g1 = out[0][1], out[1][1]
     assert (g0 - g1).norm().item() <= 2e-2 * g0.norm().item()
+
+
+@pytest.mark.parametrize("name,extra", CASES)
+def test_batched_finalizes_are_bitwise_identical(name, extra):
+    """Bias / LayerNorm gradient finalizes queued during the backward and launched together
+    (ops/functional.py flush_finalizes) give bit-for-bit the gradients of one launch each, with
+    DDP's reducer in the loop (its bucket launches and end-of-backward flush)."""
+    from distributed_training_and_deepspeed_amd.ops import functional as Fx
+    from distributed_training_and_deepspeed_amd.parallel import DistributedDataParallel
+    cfg = C.get_config(name).with_(**extra)
+    C.PRESETS["_t"] = cfg
+    grads = {}
+    for batched in (False, True):
+        Fx.set_finalize_batching(batched)
+        try:
+            model = build_model("_t", impl="fused", seed=3, device="cuda", dtype=torch.bfloat16)
+            ddp = DistributedDataParallel(model, bucket_cap_mb=0.05)
+            ds = SyntheticLMDataset(cfg, 4, seq_len=128, seed=5)
+            loss = ddp(ds.input_ids.cuda(), labels=ds.labels.cuda()).loss
+            loss.backward()
+            assert not Fx._PENDING
+            grads[batched] = [p.grad.detach().clone() for p in model.parameters()]
+        finally:
+            Fx.set_finalize_batching(True)
+    for g0, g1 in zip(grads[False], grads[True]):
+        assert torch.equal(g0, g1)
