@@ -200,6 +200,13 @@ def emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, async_ok: boo
     grad_done(p)
 
 
+# Token count from which the weight gradients take wgrad.hip (below: hipBLASLt, split-K bmm from
+# 8192, one GEMM under it); DTD_WGRAD_MIN_T.  At the reference's small batches the kernel loses:
+# b4 graph 352-354 k vs 384-385 k tokens/s, bloom-560m b1 37.7 k vs 42.0 k with T >= 512
+# (profiles/r6_wgrad_min_t.jsonl).
+_WGRAD_MIN_T = [int(os.environ.get("DTD_WGRAD_MIN_T", "8192"))]
+
+
 def _emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
     dst, acc = grad_dst(p)
     T, o = dy.shape
@@ -210,7 +217,7 @@ def _emit_wgrad(p: torch.Tensor, dy: torch.Tensor, x: torch.Tensor) -> None:
             # reference-precision path: the f32-MFMA TN kernel, fp32 split-K partials
             splitk_reduce(G.gemm_f32_tn(dy, x), dst, acc)
             return
-    if dy.is_cuda and T >= 8192:
+    if dy.is_cuda and T >= _WGRAD_MIN_T[0]:
         from . import gemm as G
         if G.wgrad_enabled() and G.wgrad_supported(dy, x):
             # ring-pipelined TN MFMA kernel (ops/csrc/wgrad.hip): fp32 split-K partials, one wave
