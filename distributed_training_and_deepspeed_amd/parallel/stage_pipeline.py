@@ -123,7 +123,7 @@ class StagePipeline(nn.Module):
 
     def __init__(self, modules, stage: int, num_stages: int, device, act_shape, act_dtype, loss_fn=None,
                  chunks: int = 1, schedule: str = "gpipe", group=None, set_micro=None, checkpoint: str = "never",
-                 loss_weighting: str = "tokens", ignore_index: int = -100):
+                 loss_weighting: str = "tokens", ignore_index: int = -100, overlap: bool = True):
         super().__init__()
         if schedule not in ("gpipe", "1f1b"):
             raise ValueError(schedule)
@@ -131,6 +131,8 @@ class StagePipeline(nn.Module):
             raise ValueError(checkpoint)
         if loss_weighting not in ("tokens", "mean"):
             raise ValueError(loss_weighting)
+        if not overlap and schedule != "gpipe":
+            raise ValueError("the blocking form (overlap=False) is a GPipe measurement baseline")
         self.mods = nn.ModuleList(modules)
         self.stage, self.num_stages = stage, num_stages
         self.device = torch.device(device)
@@ -140,6 +142,9 @@ class StagePipeline(nn.Module):
         self.set_micro = set_micro
         self.checkpoint = checkpoint
         self.loss_weighting, self.ignore_index = loss_weighting, ignore_index
+        # overlap=False: the blocking form (each receive posted at its consumer and waited there,
+        # each send waited right after it) -- kept to measure what the overlap buys
+        self.overlap = bool(overlap)
         self.link = _Link(group)
         self.first = stage == 0
         self.last = stage == num_stages - 1
@@ -211,15 +216,24 @@ class StagePipeline(nn.Module):
         def send_fwd(y):
             if not self.last:
                 self.link.isend(y, s + 1)
+                if not self.overlap:
+                    self.link.drain()
 
         def send_bwd(gx):
             if not self.first:
                 self.link.isend(gx, s - 1)
+                if not self.overlap:
+                    self.link.drain()
 
         def take(r):
             return None if r is None else r.wait()
 
-        if self.schedule == "gpipe":
+        if self.schedule == "gpipe" and not self.overlap:   # the blocking form
+            for m in range(n):
+                send_fwd(forward(m, take(post_fwd(m))))
+            for k in range(n):
+                send_bwd(backward(take(post_bwd(k))))
+        elif self.schedule == "gpipe":
             nxt = post_fwd(0)
             for m in range(n):
                 cur, nxt = nxt, post_fwd(m + 1)

@@ -86,6 +86,8 @@ def main():
                         help="replay the whole step (every stage's micro-batch forwards and backwards, loss, "
                              "optimizer) as one hipGraph when all stages share one GPU; auto: on then, unless "
                              "--verbose (whose per-hook prints need eager steps)")
+    parser.add_argument("--pipe-overlap", default="on", choices=["on", "off"],
+                        help="stage-per-process: off = the blocking send/recv form (a GPipe measurement baseline)")
     parser.add_argument("--pipe-backend", default="auto", choices=["auto", "rccl", "gloo"],
                         help="stage-per-process mode (launched with several ranks): the point-to-point "
                              "transport; auto = RCCL on GPUs, gloo on CPU")
@@ -227,7 +229,7 @@ def main_stage_per_process(args):
     pipe = StagePipeline(mods, rank, world, device, act_shape=lambda mb: (mb, args.seq_len, config.hidden_size),
                          act_dtype=dtype, loss_fn=lambda out, t: loss_fn(_flat(out, upcast), t.reshape(-1)),
                          chunks=chunks, schedule=args.schedule, set_micro=lambda m: setattr(owner.rt.rng, "micro", m),
-                         checkpoint=ck if args.pipeline else "never")
+                         checkpoint=ck if args.pipeline else "never", overlap=args.pipe_overlap == "on")
     optimizer = torch_adamw([p for p in pipe.parameters() if p.requires_grad], lr=5e-5)
     dataset = load_synthetic(config, args.batch_size * args.training_steps, seq_len=args.seq_len, seed=0)
     g = torch.Generator().manual_seed(0)
@@ -291,7 +293,7 @@ def main_stage_per_process(args):
         print(json.dumps({"tokens_per_s": round(n * args.batch_size * args.seq_len / max(elapsed, 1e-9), 1),
                           "timed_steps": n, "graph": graphed is not None, "pipeline": args.pipeline,
                           "schedule": args.schedule if args.pipeline else None, "stages": world,
-                          "mode": "stage-per-process", "transport": backend,
+                          "mode": "stage-per-process", "transport": backend, "overlap": args.pipe_overlap,
                           "checkpoint": ck if args.pipeline else None,
                           "idle_ms_per_step": [None if v is None else round(v, 3) for v in idle_all],
                           "final_loss": loss_all[-1]}))

@@ -34,7 +34,8 @@ def _loss(cfg):
     return lambda out, t: ce(out.reshape(-1, cfg.vocab_size).float(), t.reshape(-1))
 
 
-def _worker(rank, world, port, out_dir, schedule, device, impl="reference", checkpoint="never", weighting="tokens"):
+def _worker(rank, world, port, out_dir, schedule, device, impl="reference", checkpoint="never", weighting="tokens",
+            overlap=True):
     import torch.distributed as dist
     from distributed_training_and_deepspeed_amd.parallel.stage_pipeline import StagePipeline, bert_stage
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -47,7 +48,7 @@ def _worker(rank, world, port, out_dir, schedule, device, impl="reference", chec
     ids, labels = _batch(cfg)
     pipe = StagePipeline(mods, rank, world, dev, act_shape=lambda mb: (mb, ids.shape[1], cfg.hidden_size),
                          act_dtype=torch.float32, loss_fn=_loss(cfg), chunks=4, schedule=schedule,
-                         checkpoint=checkpoint, loss_weighting=weighting)
+                         checkpoint=checkpoint, loss_weighting=weighting, overlap=overlap)
     loss = pipe.train_step(ids.to(dev) if rank == 0 else None, labels.to(dev) if rank == world - 1 else None,
                            rows=ids.shape[0])
     names = {id(p): n for n, p in owner.named_parameters()}
@@ -97,13 +98,14 @@ def test_micro_loss_weights_sum_to_the_concatenated_loss():
     assert torch.allclose(parts, ce(logits.reshape(-1, 10), labels.reshape(-1)), rtol=1e-5)
 
 
-@pytest.mark.parametrize("world,schedule,checkpoint,weighting", [
-    (2, "gpipe", "never", "tokens"), (2, "1f1b", "never", "tokens"), (3, "gpipe", "never", "tokens"),
-    (3, "1f1b", "never", "tokens"), (2, "gpipe", "except_last", "tokens"), (3, "1f1b", "except_last", "tokens"),
-    (2, "1f1b", "always", "tokens"), (2, "gpipe", "never", "mean")])
-def test_stage_per_process_matches_sequential(tmp_path, world, schedule, checkpoint, weighting):
+@pytest.mark.parametrize("world,schedule,checkpoint,weighting,overlap", [
+    (2, "gpipe", "never", "tokens", True), (2, "1f1b", "never", "tokens", True), (3, "gpipe", "never", "tokens", True),
+    (3, "1f1b", "never", "tokens", True), (2, "gpipe", "except_last", "tokens", True),
+    (3, "1f1b", "except_last", "tokens", True), (2, "1f1b", "always", "tokens", True),
+    (2, "gpipe", "never", "mean", True), (3, "gpipe", "never", "tokens", False)])
+def test_stage_per_process_matches_sequential(tmp_path, world, schedule, checkpoint, weighting, overlap):
     mp.spawn(_worker, args=(world, pick_free_port(), str(tmp_path), schedule, "cpu", "reference", checkpoint,
-                            weighting), nprocs=world, join=True)
+                            weighting, overlap), nprocs=world, join=True)
     ref, ref_loss = _sequential(weighting)
     seen = set()
     for r in range(world):
