@@ -37,14 +37,21 @@ def _transfer(x: torch.Tensor, dst: torch.device) -> torch.Tensor:
     src_stream = torch.cuda.current_stream(src)
     ready = torch.cuda.Event()
     ready.record(src_stream)          # x is produced on the source compute stream
+    # y is allocated on the destination's compute stream -- its consumer -- so the allocator
+    # recycles it in that stream's order and it needs no record_stream; that stream waits for
+    # the copy below before anything reads y
+    with torch.cuda.device(dst):
+        y = torch.empty(x.shape, dtype=x.dtype, device=dst)
     with torch.cuda.device(dst), torch.cuda.stream(cs):
         cs.wait_event(ready)
-        y = x.to(dst, non_blocking=True)
-    x.record_stream(cs)               # keep x alive until the copy finished
+        y.copy_(x, non_blocking=True)
+    # x belongs to the source stream's pool; the copy stream's read must finish before the
+    # allocator hands x's block out again: one record_stream per transfer (two per micro-batch
+    # and stage boundary, not per kernel -- not the per-tensor pattern that slowed --async-wgrad)
+    x.record_stream(cs)
     done = torch.cuda.Event()
     done.record(cs)
     torch.cuda.current_stream(dst).wait_event(done)
-    y.record_stream(torch.cuda.current_stream(dst))
     return y
 
 
