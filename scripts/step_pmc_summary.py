@@ -17,7 +17,7 @@ from collections import defaultdict
 def family(name: str) -> str:
     if "Cijk" in name:
         return "hipBLASLt GEMM"
-    m = re.search(r"(gemm_bt_persistent<\d+|gemm_f32_kernel<\w+>|wgrad_tn_kernel|gemm_tn\w*|attn_\w+_kernel\w*|ln_\w+_wave|emb_ln_fwd_wave|adam_kernel|xent_\w+_kernel|"
+    m = re.search(r"(gemm_bt_persistent<\d+|gemm_w4_kernel<\d+|gemm_f32_kernel<\w+>|wgrad_tn_kernel|gemm_tn\w*|attn_\w+_kernel\w*|ln_\w+_wave|emb_ln_fwd_wave|adam_kernel|xent_\w+_kernel|"
                   r"splitk_reduce_kernel|embed_\w+_kernel|colsum_finalize_kernel|act_\w+_kernel|dropout_kernel)", name)
     return m.group(1) if m else "other"
 
