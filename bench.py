@@ -108,6 +108,17 @@ def parse():
     return ap.parse_args()
 
 
+def _hand_gemm_config() -> dict:
+    """Which products the hand-written GEMMs take in this run (ops/gemm.py dispatch rules)."""
+    from distributed_training_and_deepspeed_amd.ops import gemm as G
+    from distributed_training_and_deepspeed_amd.ops import functional as Fx
+    from distributed_training_and_deepspeed_amd.ops import grad as GR
+    return {"proj_w4": G.w4_enabled(), "proj_w4_max_k": G._W4_MAX_K[0], "proj_w4_min_tiles": G.w4_min_tiles(),
+            "proj_w4_residual_add": G._W4_ADD[0], "ffn_fused": G.ffn_fwd_enabled(),
+            "ffn_min_tiles": G._FFN_MIN_TILES[0] or "cus", "wgrad": G.wgrad_enabled(),
+            "wgrad_min_tokens": GR._WGRAD_MIN_T[0], "finalize_batch": Fx._BATCH[0]}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -314,6 +325,7 @@ def main():
                 "optimizer": ("fused Adam on the ZeRO shard (zero_dp_training.py config, lr 1.5e-4)" if zero
                               else "fused AdamW (transformers.AdamW hyper-params, lr 5e-5)"),
                 "tuned_gemms": tuned,
+                "hand_gemms": _hand_gemm_config() if cuda else None,
                 "hip_graph": graphed is not None,
                 "force_collectives": args.force_collectives,
                 "prewarm": args.prewarm,
