@@ -368,7 +368,7 @@ class _LMHeadFn(torch.autograd.Function):
         w = ctx.head.weight
         dlogits = Fx.xent_bwd(logits, labels, lse, stats, gloss)
         emit_wgrad(w, dlogits, x)
-        return dlogits @ w, None, None, None
+        return G.head_dgrad(dlogits, w), None, None, None
 
 
 class LMHead(nn.Module):

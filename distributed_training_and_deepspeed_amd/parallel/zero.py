@@ -513,11 +513,11 @@ class ZeroEngine(nn.Module):
                     p.main_grad = s.view(s.gbuf, i)
                 off += s.numel
         # ring arenas: gradient landing regions (stages 2/3) and gathered units (stage 3)
-        # (aliased stage-3 units land in their own shard and gather nothing: no arena for them).
+        # (aliased stage-3 segments land in their own shard and gather nothing: no arena for them).
         # The landing arena never exceeds the regions it can hold at once -- the whole gradient
         # -- so a large reduce_bucket_size on a small model does not pin more than that.
         reg = [s.numel for s in self.segments
-               if (s.unit and not self.alias_units) or (not s.unit and self.stage >= 2 and not self.replicated)]
+               if not self.alias_units and (s.unit or (self.stage >= 2 and not self.replicated))]
         big_unit = 0 if self.alias_units else max([s.numel for s in self.units], default=0)
         want = max(4 * max(self.config.reduce_bucket, ALIGN), 3 * big_unit)
         self.landing = _Arena(min(want, sum(reg)) if reg else 0, self.grad_dtype, dev)
@@ -550,6 +550,16 @@ class ZeroEngine(nn.Module):
             self.lowp_view = self.master
         else:
             self.lowp_view = self.lowp
+        if self.alias_units:
+            # one rank, stage 3: the persistent buckets alias their (whole) shard as the units do, so
+            # their gradients land in place and the refresh copies nothing.  bloom-560m's tied
+            # 257 M-parameter embedding paid a landing copy + a refresh copy, 0.4 ms of a 12.4 ms
+            # step (profiles/r6_bloom_z3_b1_kernels.txt)
+            for s in self.buckets:
+                s.full = self.lowp_view[s.shard_off:s.shard_off + s.numel]
+                for i, p in enumerate(s.params):
+                    p.data = s.view(s.full, i)
+            self.param_flat = torch.empty(0, dtype=dt, device=dev)
 
     def _set_released(self, s: _Segment) -> None:
         for p in s.params:
@@ -607,7 +617,7 @@ class ZeroEngine(nn.Module):
             self._alloc_landing(s)
 
     def _alloc_landing(self, s: _Segment) -> None:
-        if s.unit and self.alias_units:   # the unit's gradient shard itself (padding stays zero)
+        if self.alias_units:   # the segment's gradient shard itself (padding stays zero)
             s.gbuf = self.gshard[s.shard_off:s.shard_off + s.numel]
             for i, p in enumerate(s.params):
                 p.main_grad = s.view(s.gbuf, i)
@@ -717,7 +727,7 @@ class ZeroEngine(nn.Module):
                         w.wait()
                     if self.backend != "nccl":
                         dst.div_(self.world)
-                elif dst.data_ptr() != buf.data_ptr():   # aliased stage-3 unit: already in place
+                elif dst.data_ptr() != buf.data_ptr():   # aliased stage-3 segment: already in place
                     dst.copy_(buf)
                 if not first:
                     out.add_(dst)
@@ -731,7 +741,7 @@ class ZeroEngine(nn.Module):
                 ev = torch.cuda.Event()
                 ev.record(cs)
         if landed:
-            if not (s.unit and self.alias_units):
+            if not self.alias_units:
                 self.landing.release(buf, ev, cs)
             s.gbuf = None
             for p in s.params:
@@ -1001,7 +1011,7 @@ class ZeroEngine(nn.Module):
         refresh each group records an event and the next forward's unit pre-hooks wait for their
         own buckets only; otherwise the compute stream waits for everything here.  Stage 3 units
         stay sharded until their next use."""
-        if self.replicated:
+        if self.replicated or self.alias_units:
             for s in self.buckets:
                 src = self.lowp_view[s.shard_off:s.shard_off + s.chunk]
                 if src.data_ptr() != s.full.data_ptr():   # aliased (the usual case): nothing to copy
