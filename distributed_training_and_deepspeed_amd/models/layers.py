@@ -391,9 +391,14 @@ class LMHead(nn.Module):
     def loss(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         """HF causal-LM loss: logits[:, :-1] vs labels[:, 1:], ignore_index -100."""
         B, S, h = x.shape
-        xs = x[:, :-1].reshape(-1, h)
-        ls = labels[:, 1:].reshape(-1)
         if self.rt.use_fused(x):
             note_use((self.weight,))
-            return _LMHeadFn.apply(xs.contiguous(), ls.contiguous(), self, self.weight)
+            # all B*S positions (tile-aligned head GEMMs, no sliced copy): each sequence's last
+            # position has no next token and takes label -100 -- zero loss and gradient, and the mean
+            # runs over the same labelled rows.  bloom-560m b1: 512 instead of 511 rows makes the
+            # logits / weight-gradient GEMMs 251 / 376 us vs 292 / 426 (profiles/r6_head_rows.json)
+            ls = torch.cat([labels[:, 1:], labels.new_full((B, 1), Fx.IGNORE_INDEX)], 1).reshape(-1)
+            return _LMHeadFn.apply(x.reshape(-1, h), ls, self, self.weight)
+        xs = x[:, :-1].reshape(-1, h)
+        ls = labels[:, 1:].reshape(-1)
         return F.cross_entropy(self.logits(xs).float(), ls, ignore_index=Fx.IGNORE_INDEX)
